@@ -1,0 +1,91 @@
+"""ctypes wrapper around the CPU restatement (oracle/qpd_oracle.cpp).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+``cpu_baseline`` leg of bench.py as the checker.  The product package never
+imports this module.  Also exposes the reference decoders compiled from their
+own sources (oracle/_ref, built by oracle/build_ref.sh) when that build exists.
+"""
+from __future__ import annotations
+
+import ctypes
+import glob
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libqpd_oracle.so")
+REF_DIR = os.path.join(HERE, "_ref")
+
+KIND = {"SC-LUT": 1, "SCL-LUT": 2, "FastSC-LUT": 3, "FastSCL-LUT": 4}
+
+_lib = None
+
+
+def build() -> None:
+    """Compile the CPU restatement (and the reference, when /root/reference exists)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    subprocess.run([os.path.join(HERE, "build_ref.sh")], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            subprocess.run(["make", "-s", "-C", HERE], check=True)
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        i32, i64 = ctypes.c_int32, ctypes.c_int64
+        L.orc_decode_lut.argtypes = [i32, i32, i32, i32, i32, P, P, P, P, i32, P, P, i32, P, i32, P, i64, P]
+        L.orc_decode_lut.restype = ctypes.c_int
+        L.orc_decode_sc_float.argtypes = [i32, i32, P, P, i64, P]
+        L.orc_decode_sc_float.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def decode_lut(kind: str, packed, K: int, L: int, frozen, symbols, node_type=None) -> np.ndarray:
+    """Decode int32 symbols [B, N] with the restated reference decoder ``kind``."""
+    N = packed.N
+    sym = np.ascontiguousarray(np.asarray(symbols, dtype=np.int32).reshape(-1, N))
+    B = sym.shape[0]
+    out = np.zeros((B, K), dtype=np.uint8)
+    frozen = np.ascontiguousarray(np.asarray(frozen, dtype=np.int32))
+    nt = None if node_type is None else np.ascontiguousarray(np.asarray(node_type).astype(np.int32))
+    keep = (packed.lut_f, packed.f_base, packed.lut_g, packed.g_base, packed.vcl)
+    rc = lib().orc_decode_lut(KIND[kind], N, K, L, packed.v, _ptr(frozen), _ptr(nt),
+                              _ptr(packed.lut_f), _ptr(packed.f_base), packed.f_step,
+                              _ptr(packed.lut_g), _ptr(packed.g_base), packed.g_step,
+                              _ptr(packed.vcl), packed.vcl_rows, _ptr(sym), B, _ptr(out))
+    del keep
+    if rc != 0:
+        raise RuntimeError(f"oracle decode failed rc={rc}")
+    return out
+
+
+def decode_sc_float(N: int, K: int, frozen, llr) -> np.ndarray:
+    x = np.ascontiguousarray(np.asarray(llr, dtype=np.float64).reshape(-1, N))
+    out = np.zeros((x.shape[0], K), dtype=np.uint8)
+    frozen = np.ascontiguousarray(np.asarray(frozen, dtype=np.int32))
+    rc = lib().orc_decode_sc_float(N, K, _ptr(frozen), _ptr(x), x.shape[0], _ptr(out))
+    if rc != 0:
+        raise RuntimeError(f"oracle decode failed rc={rc}")
+    return out
+
+
+def reference_module():
+    """The reference decoders compiled from /root/reference sources, or None."""
+    hits = glob.glob(os.path.join(REF_DIR, "_refPolarDecoder*.so"))
+    if not hits:
+        return None
+    if REF_DIR not in sys.path:
+        sys.path.insert(0, REF_DIR)
+    import _refPolarDecoder  # noqa: E402
+
+    return _refPolarDecoder
