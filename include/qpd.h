@@ -1,0 +1,132 @@
+/*
+ * qpd.h -- C-ABI of the MI355X quantized polar decoder (libqpd.so).
+ *
+ * The drop-in boundary for the reference's L1 decoders.  Each entry point
+ * replaces one piece of the reference's pybind11 surface
+ * (/root/reference/PolarDecoder/PolarDecoder/_cpp):
+ *
+ *   qpd_create    <- the decoder constructors, which copy every table into the
+ *                    object:  SCLUT::SCLUT        src/SCLUTDecoder.cpp:10-19
+ *                             SCLLUT::SCLLUT      src/SCLLUTDecoder.cpp:33-44
+ *                             FastSCLUT::FastSCLUT src/FastSCLUT.cpp:13-24
+ *                             FastSCLLUT::FastSCLLUT src/FastSCLLUTDecoder.cpp:42-55
+ *                             SC::SC              src/SCDecoder.cpp:7-12
+ *                   bound at py_interface/py_{SCLUT,SCLLUT,FastSCLUT,FastSCLLUT,SC}Decoder.cpp
+ *   qpd_decode    <- SCLUT::decode   src/SCLUTDecoder.cpp:21-124
+ *                    SCLLUT::decode  src/SCLLUTDecoder.cpp:47-253
+ *                    FastSCLUT::decode src/FastSCLUT.cpp:27-206
+ *                    FastSCLLUT::decode src/FastSCLLUTDecoder.cpp:57-408
+ *                   (batched: B frames per call instead of one)
+ *   qpd_decode_f64 <- SC::decode     src/SCDecoder.cpp:14-89 (float64 LLR input)
+ *   qpd_decode_host / qpd_decode_f64_host: the same from host buffers
+ *                   (copy in, decode, copy out, synchronous) -- what a
+ *                   per-frame `decode(symbols)` call needs.
+ *   qpd_destroy   <- the pybind11 object's destructor
+ *
+ * Plain pointers and sizes only; no torch or HIP types in the signatures
+ * (streams are passed as `void*` = hipStream_t, NULL = default stream).
+ *
+ * Errors: every function returns QPD_OK (0) or a negative QPD_E* code and
+ * records a message retrievable with qpd_last_error() (thread-local).  The
+ * reference performs no validation (out-of-range symbols are UB there); this
+ * library rejects bad configurations at create time and flags out-of-range
+ * channel symbols on the device (reported by the host entry points and by
+ * qpd_check_input_error()).
+ */
+#ifndef QPD_H
+#define QPD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QPD_ABI_VERSION 1
+
+/* Decoder kinds (the reference's class names). */
+enum qpd_kind {
+    QPD_SC_FLOAT = 0,    /* SCDecoder       (min-sum on float64 LLRs)        */
+    QPD_SC_LUT = 1,      /* SCLUTDecoder                                      */
+    QPD_SCL_LUT = 2,     /* SCLLUTDecoder                                     */
+    QPD_FASTSC_LUT = 3,  /* FastSCLUTDecoder  (R0/R1/REP/SPC shortcuts)       */
+    QPD_FASTSCL_LUT = 4  /* FastSCLLUTDecoder (R0/R1/REP shortcuts; no SPC)   */
+};
+
+enum qpd_status {
+    QPD_OK = 0,
+    QPD_E_INVALID = -1,     /* bad argument / configuration                  */
+    QPD_E_UNSUPPORTED = -2, /* valid for the reference, not supported here   */
+    QPD_E_DEVICE = -3,      /* HIP runtime failure                           */
+    QPD_E_INPUT = -4        /* channel symbol outside [0, v) seen on device  */
+};
+
+/*
+ * Decoder description.  All arrays are host pointers, copied at create time
+ * (the reference's ctors copy too).
+ *
+ * Tables use the packed layout (quantized_decoder_polar_codes_amd/lut.py):
+ *   f table t : lut_f[t*v*v + a*v + b]              a = first-half symbol
+ *   g table t : lut_g[(t*2 + u)*v*v + a*v + b]      u = left partial sum
+ *   node p = 2^depth + node - 1, element j of that node uses table
+ *            f_base[p] + j*f_step  (f_step = 0: one table per node)
+ *   vcl[((row*N) + pos)*v + sym], row in [0, vcl_rows)
+ */
+typedef struct qpd_config {
+    int32_t kind;               /* enum qpd_kind                                  */
+    int32_t N;                  /* code length, power of two, 2..65536            */
+    int32_t K;                  /* output bits = number of 0 entries in frozen    */
+    int32_t L;                  /* list size (SCL kinds), 1..8; ignored otherwise */
+    int32_t v;                  /* symbol alphabet size, 2..256 (LUT kinds)       */
+    const int32_t *frozen_bits; /* [N], 1 = frozen, 0 = information               */
+    const int32_t *node_type;   /* [2N-1] node labels (Fast kinds), else NULL     */
+    const uint8_t *lut_f;       /* [lut_f_count][v][v]                            */
+    int32_t lut_f_count;
+    const int32_t *f_base;      /* [N-1]                                          */
+    int32_t f_step;             /* 0 or 1                                         */
+    const uint8_t *lut_g;       /* [lut_g_count][2][v][v]                         */
+    int32_t lut_g_count;
+    const int32_t *g_base;      /* [N-1]                                          */
+    int32_t g_step;             /* 0 or 1                                         */
+    const double *vcl;          /* [vcl_rows][N][v], finite                       */
+    int32_t vcl_rows;           /* >= log2(N)                                     */
+    int32_t device;             /* HIP device ordinal (-1 = current device)       */
+    int32_t max_waves;          /* persistent-grid size cap (0 = default)         */
+} qpd_config;
+
+typedef struct qpd_decoder qpd_decoder;
+
+int qpd_abi_version(void);
+const char *qpd_last_error(void);
+
+int qpd_create(const qpd_config *cfg, qpd_decoder **out);
+void qpd_destroy(qpd_decoder *dec);
+
+/* LUT kinds.  d_symbols: device int32 [B][N]; d_out: device uint8 [B][K]. */
+int qpd_decode(qpd_decoder *dec, const int32_t *d_symbols, int64_t B, uint8_t *d_out, void *stream);
+/* QPD_SC_FLOAT.  d_llr: device float64 [B][N]; d_out: device uint8 [B][K].  */
+int qpd_decode_f64(qpd_decoder *dec, const double *d_llr, int64_t B, uint8_t *d_out, void *stream);
+
+/* Host-buffer variants (synchronous). */
+int qpd_decode_host(qpd_decoder *dec, const int32_t *h_symbols, int64_t B, uint8_t *h_out);
+int qpd_decode_f64_host(qpd_decoder *dec, const double *h_llr, int64_t B, uint8_t *h_out);
+
+/* Returns QPD_E_INPUT (and clears the flag) if any decode since the last
+ * check saw a channel symbol outside [0, v); synchronizes the device. */
+int qpd_check_input_error(qpd_decoder *dec);
+
+/* Introspection for tests / benchmarks. */
+typedef struct qpd_info {
+    int32_t kind, N, K, L, v;
+    int32_t num_ops;          /* length of the static traversal schedule     */
+    int32_t frames_per_wave;  /* frames decoded by one 64-lane wavefront     */
+    int32_t lanes_per_frame;  /* lane stride of one frame (pow2 >= L)        */
+    int32_t max_waves;        /* persistent grid cap                         */
+    int64_t scratch_bytes_per_wave;
+} qpd_info;
+int qpd_get_info(const qpd_decoder *dec, qpd_info *info);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QPD_H */

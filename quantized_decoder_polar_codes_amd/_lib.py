@@ -1,0 +1,126 @@
+"""ctypes binding of libqpd.so (the C-ABI declared in include/qpd.h).
+
+The library is built in-tree by :func:`quantized_decoder_polar_codes_amd.build.build_native`
+(hipcc --offload-arch=gfx950).  There is no fallback: if the library is
+missing, or no HIP device is present, decoding raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libqpd.so")
+
+QPD_SC_FLOAT, QPD_SC_LUT, QPD_SCL_LUT, QPD_FASTSC_LUT, QPD_FASTSCL_LUT = range(5)
+QPD_OK, QPD_E_INVALID, QPD_E_UNSUPPORTED, QPD_E_DEVICE, QPD_E_INPUT = 0, -1, -2, -3, -4
+
+# Every symbol include/qpd.h declares (tests check the library exports them).
+EXPORTED = (
+    "qpd_abi_version",
+    "qpd_last_error",
+    "qpd_create",
+    "qpd_destroy",
+    "qpd_decode",
+    "qpd_decode_f64",
+    "qpd_decode_host",
+    "qpd_decode_f64_host",
+    "qpd_check_input_error",
+    "qpd_get_info",
+)
+
+_P = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+
+
+class QpdConfig(ctypes.Structure):
+    _fields_ = [
+        ("kind", _i32),
+        ("N", _i32),
+        ("K", _i32),
+        ("L", _i32),
+        ("v", _i32),
+        ("frozen_bits", _P),
+        ("node_type", _P),
+        ("lut_f", _P),
+        ("lut_f_count", _i32),
+        ("f_base", _P),
+        ("f_step", _i32),
+        ("lut_g", _P),
+        ("lut_g_count", _i32),
+        ("g_base", _P),
+        ("g_step", _i32),
+        ("vcl", _P),
+        ("vcl_rows", _i32),
+        ("device", _i32),
+        ("max_waves", _i32),
+    ]
+
+
+class QpdInfo(ctypes.Structure):
+    _fields_ = [
+        ("kind", _i32),
+        ("N", _i32),
+        ("K", _i32),
+        ("L", _i32),
+        ("v", _i32),
+        ("num_ops", _i32),
+        ("frames_per_wave", _i32),
+        ("lanes_per_frame", _i32),
+        ("max_waves", _i32),
+        ("scratch_bytes_per_wave", _i64),
+    ]
+
+
+_lib = None
+
+
+class QpdError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libqpd error {code}: {msg}")
+        self.code = code
+
+
+def load():
+    """Load libqpd.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)"
+        )
+    L = ctypes.CDLL(LIB_PATH)
+    L.qpd_abi_version.restype = ctypes.c_int
+    L.qpd_last_error.restype = ctypes.c_char_p
+    L.qpd_create.argtypes = [ctypes.POINTER(QpdConfig), ctypes.POINTER(_P)]
+    L.qpd_create.restype = ctypes.c_int
+    L.qpd_destroy.argtypes = [_P]
+    L.qpd_destroy.restype = None
+    L.qpd_decode.argtypes = [_P, _P, _i64, _P, _P]
+    L.qpd_decode.restype = ctypes.c_int
+    L.qpd_decode_f64.argtypes = [_P, _P, _i64, _P, _P]
+    L.qpd_decode_f64.restype = ctypes.c_int
+    L.qpd_decode_host.argtypes = [_P, _P, _i64, _P]
+    L.qpd_decode_host.restype = ctypes.c_int
+    L.qpd_decode_f64_host.argtypes = [_P, _P, _i64, _P]
+    L.qpd_decode_f64_host.restype = ctypes.c_int
+    L.qpd_check_input_error.argtypes = [_P]
+    L.qpd_check_input_error.restype = ctypes.c_int
+    L.qpd_get_info.argtypes = [_P, ctypes.POINTER(QpdInfo)]
+    L.qpd_get_info.restype = ctypes.c_int
+    if L.qpd_abi_version() != 1:
+        raise ImportError("libqpd.so ABI version mismatch")
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc == QPD_OK:
+        return
+    msg = load().qpd_last_error().decode(errors="replace")
+    if rc in (QPD_E_INVALID, QPD_E_UNSUPPORTED, QPD_E_INPUT):
+        raise ValueError(msg)
+    raise QpdError(rc, msg)

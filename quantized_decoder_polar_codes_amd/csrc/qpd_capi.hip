@@ -1,0 +1,411 @@
+// qpd_capi.hip -- C-ABI of libqpd.so (include/qpd.h): validation, the static
+// traversal-schedule compiler, device residency of the tables and kernel
+// launches.  Host code only; kernels in qpd_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "qpd.h"
+#include "qpd_kernels.hip"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define QPD_HIP(call)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (call);                                                              \
+        if (e_ != hipSuccess) return fail(QPD_E_DEVICE, std::string(#call ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+using qpd::DevPlan;
+using qpd::Op;
+
+int ilog2_exact(int N) {
+    int n = 0;
+    while ((1 << n) < N) ++n;
+    return ((1 << n) == N) ? n : -1;
+}
+
+// Static traversal schedule.  The reference walks the
+// tree with a node_state machine (src/SCLLUTDecoder.cpp:62-243); the walk does
+// not depend on data, so it is compiled once per code into a flat op list that
+// every frame replays.  Special nodes follow node_type AS PASSED (H7):
+// FastSC-LUT handles R0/R1/REP/SPC (FastSCLUT.cpp:46-107), FastSCL-LUT handles
+// R0/R1/REP only (FastSCLLUTDecoder.cpp:82-215); other labels decode as plain
+// f/g nodes.
+struct Schedule {
+    std::vector<Op> ops;
+    int max_r1 = 0;
+};
+
+int special_of(int kind, const int32_t *node_type, int posi) {
+    if (!node_type) return -1;
+    const int t = node_type[posi];
+    if (kind == QPD_FASTSC_LUT && t >= 0 && t <= 3) return t;
+    if (kind == QPD_FASTSCL_LUT && t >= 0 && t <= 2) return t;
+    return -1;
+}
+
+void emit(Schedule &s, int type, int d, int node, int aux) {
+    Op op;
+    op.type = type;
+    op.d = d;
+    op.node = node;
+    op.aux = aux;
+    s.ops.push_back(op);
+}
+
+void visit(Schedule &s, int kind, int N, int n, const int32_t *frozen, const int32_t *node_type, int d, int node) {
+    const int posi = (1 << d) + node - 1;
+    const int t = special_of(kind, node_type, posi);
+    if (t >= 0) {
+        emit(s, qpd::OP_R0 + t, d, node, 0);
+        if (t == 1) s.max_r1 = std::max(s.max_r1, N >> d);
+        return;
+    }
+    if (d + 1 < n) {
+        emit(s, qpd::OP_F, d, node, 0);
+        visit(s, kind, N, n, frozen, node_type, d + 1, 2 * node);
+        emit(s, qpd::OP_G, d, node, 0);
+        visit(s, kind, N, n, frozen, node_type, d + 1, 2 * node + 1);
+    } else {
+        emit(s, qpd::OP_LEAF_L, d, node, frozen[2 * node] == 1);
+        emit(s, qpd::OP_LEAF_R, d, node, frozen[2 * node + 1] == 1);
+    }
+    emit(s, qpd::OP_COMB, d, node, 0);
+}
+
+struct DeviceBuf {
+    void *p = nullptr;
+    ~DeviceBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+}  // namespace
+
+struct qpd_decoder {
+    int kind, N, n, K, L, v, device;
+    int max_waves;
+    int64_t scratch_bytes_per_wave;
+    DevPlan plan{};
+    std::vector<Op> ops_host;
+    DeviceBuf lut_f, f_base, lut_g, g_base, vcl, ops, info_pos, scratch, err;
+    // staging for the host-buffer entry points
+    DeviceBuf h_in, h_out;
+    size_t h_in_bytes = 0, h_out_bytes = 0;
+};
+
+namespace {
+
+template <class T>
+int upload(DeviceBuf &b, const T *src, size_t count) {
+    const size_t bytes = std::max<size_t>(1, count * sizeof(T));
+    QPD_HIP(hipMalloc(&b.p, bytes));
+    if (count) QPD_HIP(hipMemcpy(b.p, src, count * sizeof(T), hipMemcpyHostToDevice));
+    return QPD_OK;
+}
+
+int set_device(const qpd_decoder *d) {
+    if (d->device >= 0) QPD_HIP(hipSetDevice(d->device));
+    return QPD_OK;
+}
+
+int validate(const qpd_config *c, int *n_out) {
+    if (!c) return fail(QPD_E_INVALID, "null config");
+    if (c->kind < QPD_SC_FLOAT || c->kind > QPD_FASTSCL_LUT) return fail(QPD_E_INVALID, "unknown decoder kind");
+    const int n = ilog2_exact(c->N);
+    if (c->N < 2 || n < 0 || n > qpd::kMaxDepth) return fail(QPD_E_INVALID, "N must be a power of two in [2, 65536]");
+    if (!c->frozen_bits) return fail(QPD_E_INVALID, "frozen_bits is NULL");
+    int zeros = 0;
+    for (int i = 0; i < c->N; ++i) {
+        if (c->frozen_bits[i] != 0 && c->frozen_bits[i] != 1)
+            return fail(QPD_E_INVALID, "frozen_bits entries must be 0 or 1");
+        zeros += c->frozen_bits[i] == 0;
+    }
+    if (zeros != c->K) return fail(QPD_E_INVALID, "K must equal the number of information (0) entries of frozen_bits");
+    *n_out = n;
+    if (c->kind == QPD_SC_FLOAT) return QPD_OK;
+    const bool list = c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT;
+    if (list && (c->L < 1 || c->L > qpd::kMaxL))
+        return fail(QPD_E_UNSUPPORTED, "list size L must be in [1, 8] (2L <= 16: libstdc++ insertion-sort regime)");
+    if (c->v < 2 || c->v > 256) return fail(QPD_E_INVALID, "alphabet size v must be in [2, 256]");
+    if (!c->lut_f || !c->lut_g || !c->f_base || !c->g_base || !c->vcl) return fail(QPD_E_INVALID, "null table pointer");
+    if ((c->f_step != 0 && c->f_step != 1) || (c->g_step != 0 && c->g_step != 1))
+        return fail(QPD_E_INVALID, "f_step/g_step must be 0 or 1");
+    if (c->vcl_rows < n) return fail(QPD_E_INVALID, "vcl_rows must be >= log2(N)");
+    const int vv = c->v * c->v;
+    for (int p = 0; p < c->N - 1; ++p) {
+        const int depth = 31 - __builtin_clz((unsigned)(p + 1));
+        const int last = (c->N >> (depth + 1)) - 1;
+        const long fl = (long)c->f_base[p] + (long)last * c->f_step;
+        const long gl = (long)c->g_base[p] + (long)last * c->g_step;
+        if (c->f_base[p] < 0 || fl >= c->lut_f_count) return fail(QPD_E_INVALID, "f_base/f_step index outside lut_f");
+        if (c->g_base[p] < 0 || gl >= c->lut_g_count) return fail(QPD_E_INVALID, "g_base/g_step index outside lut_g");
+    }
+    for (long i = 0; i < (long)c->lut_f_count * vv; ++i)
+        if (c->lut_f[i] >= c->v) return fail(QPD_E_INVALID, "lut_f entry outside [0, v)");
+    for (long i = 0; i < (long)c->lut_g_count * 2 * vv; ++i)
+        if (c->lut_g[i] >= c->v) return fail(QPD_E_INVALID, "lut_g entry outside [0, v)");
+    for (long i = 0; i < (long)n * c->N * c->v; ++i)
+        if (!std::isfinite(c->vcl[i])) return fail(QPD_E_INVALID, "vcl rows 0..n-1 must be finite");
+    if (c->kind == QPD_FASTSC_LUT || c->kind == QPD_FASTSCL_LUT) {
+        if (!c->node_type) return fail(QPD_E_INVALID, "node_type is required for the Fast decoders");
+        if (special_of(c->kind, c->node_type, 0) >= 0)
+            return fail(QPD_E_UNSUPPORTED, "root node labelled special (undefined behaviour in the reference)");
+    }
+    return QPD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qpd_abi_version(void) { return QPD_ABI_VERSION; }
+
+const char *qpd_last_error(void) { return g_err.c_str(); }
+
+int qpd_create(const qpd_config *c, qpd_decoder **out) {
+    if (!out) return fail(QPD_E_INVALID, "null output handle");
+    *out = nullptr;
+    int n = 0;
+    int rc = validate(c, &n);
+    if (rc) return rc;
+    if (c->device >= 0) QPD_HIP(hipSetDevice(c->device));
+
+    qpd_decoder *d = new qpd_decoder();
+    d->kind = c->kind;
+    d->N = c->N;
+    d->n = n;
+    d->K = c->K;
+    const bool list = c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT;
+    d->L = list ? c->L : 1;
+    d->v = c->kind == QPD_SC_FLOAT ? 0 : c->v;
+    d->device = c->device;
+
+    Schedule s;
+    visit(s, c->kind, c->N, n, c->frozen_bits, (c->kind == QPD_FASTSC_LUT || c->kind == QPD_FASTSCL_LUT) ? c->node_type : nullptr, 0, 0);
+    d->ops_host = s.ops;
+
+    DevPlan &P = d->plan;
+    P.N = c->N;
+    P.n = n;
+    P.K = c->K;
+    P.L = d->L;
+    P.v = d->v;
+    int gs = 1;
+    while (gs < d->L) gs *= 2;
+    P.gs = gs;
+    P.fpw = 64 / gs;
+    P.nops = (int)s.ops.size();
+    P.max_r1 = s.max_r1;
+    // scratch layout, in 64-lane dword rows
+    int r = 0;
+    const int N = c->N;
+    for (int dd = 0; dd <= qpd::kMaxDepth; ++dd) P.So[dd] = P.Uo[dd] = 0;
+    for (int dd = 1; dd <= n - 1; ++dd) {
+        P.So[dd] = r;
+        r += c->kind == QPD_SC_FLOAT ? 2 * (N >> dd) : std::max(1, ((N >> dd) + 3) / 4);
+    }
+    for (int dd = 1; dd <= n; ++dd) {
+        P.Uo[dd] = r;
+        r += std::max(1, ((N >> dd) + 31) / 32);
+    }
+    P.Ro = r;
+    r += std::max(1, (N + 31) / 32);
+    P.Ho = P.Ko = P.Io = r;
+    if (c->kind == QPD_FASTSCL_LUT && s.max_r1 > 0) {
+        P.Ho = r;
+        r += (s.max_r1 + 31) / 32;
+        P.Ko = r;
+        r += 2 * s.max_r1;
+        P.Io = r;
+        if (s.max_r1 > qpd::stl::kThreshold) r += s.max_r1;
+    }
+    P.rows_per_wave = r;
+    P.f_step = c->f_step;
+    P.g_step = c->g_step;
+    d->scratch_bytes_per_wave = (int64_t)r * 64 * 4;
+    int mw = c->max_waves > 0 ? c->max_waves : 256 * 8;
+    const int64_t cap = (int64_t)2 << 30;  // <= 2 GiB of scratch
+    mw = (int)std::max<int64_t>(1, std::min<int64_t>(mw, cap / d->scratch_bytes_per_wave));
+    d->max_waves = mw;
+
+    std::vector<int32_t> info;
+    for (int i = 0; i < N; ++i)
+        if (c->frozen_bits[i] == 0) info.push_back(i);
+
+#define QPD_TRY(x)            \
+    do {                      \
+        int rc_ = (x);        \
+        if (rc_) {            \
+            delete d;         \
+            return rc_;       \
+        }                     \
+    } while (0)
+    QPD_TRY(upload(d->ops, s.ops.data(), s.ops.size()));
+    QPD_TRY(upload(d->info_pos, info.data(), info.size()));
+    if (c->kind != QPD_SC_FLOAT) {
+        const size_t vv = (size_t)c->v * c->v;
+        QPD_TRY(upload(d->lut_f, c->lut_f, (size_t)c->lut_f_count * vv));
+        QPD_TRY(upload(d->lut_g, c->lut_g, (size_t)c->lut_g_count * 2 * vv));
+        QPD_TRY(upload(d->f_base, c->f_base, (size_t)N - 1));
+        QPD_TRY(upload(d->g_base, c->g_base, (size_t)N - 1));
+        QPD_TRY(upload(d->vcl, c->vcl, (size_t)c->vcl_rows * N * c->v));
+    }
+    {
+        hipError_t e = hipMalloc(&d->scratch.p, (size_t)d->scratch_bytes_per_wave * mw);
+        if (e != hipSuccess) {
+            delete d;
+            return fail(QPD_E_DEVICE, std::string("scratch hipMalloc: ") + hipGetErrorString(e));
+        }
+        e = hipMalloc(&d->err.p, sizeof(int32_t));
+        if (e == hipSuccess) e = hipMemset(d->err.p, 0, sizeof(int32_t));
+        if (e != hipSuccess) {
+            delete d;
+            return fail(QPD_E_DEVICE, std::string("err hipMalloc: ") + hipGetErrorString(e));
+        }
+    }
+#undef QPD_TRY
+    P.lut_f = (const uint8_t *)d->lut_f.p;
+    P.f_base = (const int32_t *)d->f_base.p;
+    P.lut_g = (const uint8_t *)d->lut_g.p;
+    P.g_base = (const int32_t *)d->g_base.p;
+    P.vcl = (const double *)d->vcl.p;
+    P.ops = (const Op *)d->ops.p;
+    P.info_pos = (const int32_t *)d->info_pos.p;
+    P.scratch = (uint32_t *)d->scratch.p;
+    P.err = (int32_t *)d->err.p;
+    *out = d;
+    return QPD_OK;
+}
+
+void qpd_destroy(qpd_decoder *d) { delete d; }
+
+int qpd_get_info(const qpd_decoder *d, qpd_info *info) {
+    if (!d || !info) return fail(QPD_E_INVALID, "null argument");
+    info->kind = d->kind;
+    info->N = d->N;
+    info->K = d->K;
+    info->L = d->L;
+    info->v = d->v;
+    info->num_ops = (int32_t)d->ops_host.size();
+    info->frames_per_wave = d->plan.fpw;
+    info->lanes_per_frame = d->plan.gs;
+    info->max_waves = d->max_waves;
+    info->scratch_bytes_per_wave = d->scratch_bytes_per_wave;
+    return QPD_OK;
+}
+
+int qpd_decode(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_out, void *stream) {
+    if (!d) return fail(QPD_E_INVALID, "null decoder");
+    if (d->kind == QPD_SC_FLOAT) return fail(QPD_E_INVALID, "SC float decoder takes float64 LLRs: use qpd_decode_f64");
+    if (B < 0) return fail(QPD_E_INVALID, "negative batch");
+    if (B == 0) return QPD_OK;
+    if (!d_symbols || !d_out) return fail(QPD_E_INVALID, "null buffer");
+    int rc = set_device(d);
+    if (rc) return rc;
+    const int64_t groups = (B + d->plan.fpw - 1) / d->plan.fpw;
+    const int grid = (int)std::min<int64_t>(groups, d->max_waves);
+    hipStream_t st = (hipStream_t)stream;
+    switch (d->kind) {
+        case QPD_SC_LUT:
+            hipLaunchKernelGGL(qpd::lut_decode_kernel<qpd::K_SC_LUT>, dim3(grid), dim3(64), 0, st, d->plan, d_symbols, B, d_out);
+            break;
+        case QPD_SCL_LUT:
+            hipLaunchKernelGGL(qpd::lut_decode_kernel<qpd::K_SCL_LUT>, dim3(grid), dim3(64), 0, st, d->plan, d_symbols, B, d_out);
+            break;
+        case QPD_FASTSC_LUT:
+            hipLaunchKernelGGL(qpd::lut_decode_kernel<qpd::K_FASTSC_LUT>, dim3(grid), dim3(64), 0, st, d->plan, d_symbols, B, d_out);
+            break;
+        case QPD_FASTSCL_LUT:
+            hipLaunchKernelGGL(qpd::lut_decode_kernel<qpd::K_FASTSCL_LUT>, dim3(grid), dim3(64), 0, st, d->plan, d_symbols, B, d_out);
+            break;
+        default:
+            return fail(QPD_E_INVALID, "bad kind");
+    }
+    QPD_HIP(hipGetLastError());
+    return QPD_OK;
+}
+
+int qpd_decode_f64(qpd_decoder *d, const double *d_llr, int64_t B, uint8_t *d_out, void *stream) {
+    if (!d) return fail(QPD_E_INVALID, "null decoder");
+    if (d->kind != QPD_SC_FLOAT) return fail(QPD_E_INVALID, "qpd_decode_f64 is for the SC float decoder");
+    if (B < 0) return fail(QPD_E_INVALID, "negative batch");
+    if (B == 0) return QPD_OK;
+    if (!d_llr || !d_out) return fail(QPD_E_INVALID, "null buffer");
+    int rc = set_device(d);
+    if (rc) return rc;
+    const int64_t groups = (B + 63) / 64;
+    const int grid = (int)std::min<int64_t>(groups, d->max_waves);
+    hipLaunchKernelGGL(qpd::sc_float_kernel, dim3(grid), dim3(64), 0, (hipStream_t)stream, d->plan, d_llr, B, d_out);
+    QPD_HIP(hipGetLastError());
+    return QPD_OK;
+}
+
+int qpd_check_input_error(qpd_decoder *d) {
+    if (!d) return fail(QPD_E_INVALID, "null decoder");
+    int rc = set_device(d);
+    if (rc) return rc;
+    int32_t flag = 0;
+    QPD_HIP(hipDeviceSynchronize());
+    QPD_HIP(hipMemcpy(&flag, d->err.p, sizeof(flag), hipMemcpyDeviceToHost));
+    if (flag) {
+        QPD_HIP(hipMemset(d->err.p, 0, sizeof(int32_t)));
+        return fail(QPD_E_INPUT, "channel symbol outside [0, v) in decoder input");
+    }
+    return QPD_OK;
+}
+
+static int ensure(DeviceBuf &b, size_t &have, size_t need) {
+    if (have >= need) return QPD_OK;
+    if (b.p) {
+        QPD_HIP(hipFree(b.p));
+        b.p = nullptr;
+    }
+    QPD_HIP(hipMalloc(&b.p, need));
+    have = need;
+    return QPD_OK;
+}
+
+int qpd_decode_host(qpd_decoder *d, const int32_t *h_symbols, int64_t B, uint8_t *h_out) {
+    if (!d) return fail(QPD_E_INVALID, "null decoder");
+    if (B <= 0) return B == 0 ? QPD_OK : fail(QPD_E_INVALID, "negative batch");
+    int rc = set_device(d);
+    if (rc) return rc;
+    const size_t in_b = (size_t)B * d->N * sizeof(int32_t), out_b = (size_t)B * d->K;
+    if ((rc = ensure(d->h_in, d->h_in_bytes, in_b))) return rc;
+    if ((rc = ensure(d->h_out, d->h_out_bytes, std::max<size_t>(1, out_b)))) return rc;
+    QPD_HIP(hipMemcpy(d->h_in.p, h_symbols, in_b, hipMemcpyHostToDevice));
+    if ((rc = qpd_decode(d, (const int32_t *)d->h_in.p, B, (uint8_t *)d->h_out.p, nullptr))) return rc;
+    if (out_b) QPD_HIP(hipMemcpy(h_out, d->h_out.p, out_b, hipMemcpyDeviceToHost));
+    return qpd_check_input_error(d);
+}
+
+int qpd_decode_f64_host(qpd_decoder *d, const double *h_llr, int64_t B, uint8_t *h_out) {
+    if (!d) return fail(QPD_E_INVALID, "null decoder");
+    if (B <= 0) return B == 0 ? QPD_OK : fail(QPD_E_INVALID, "negative batch");
+    int rc = set_device(d);
+    if (rc) return rc;
+    const size_t in_b = (size_t)B * d->N * sizeof(double), out_b = (size_t)B * d->K;
+    if ((rc = ensure(d->h_in, d->h_in_bytes, in_b))) return rc;
+    if ((rc = ensure(d->h_out, d->h_out_bytes, std::max<size_t>(1, out_b)))) return rc;
+    QPD_HIP(hipMemcpy(d->h_in.p, h_llr, in_b, hipMemcpyHostToDevice));
+    if ((rc = qpd_decode_f64(d, (const double *)d->h_in.p, B, (uint8_t *)d->h_out.p, nullptr))) return rc;
+    if (out_b) QPD_HIP(hipMemcpy(h_out, d->h_out.p, out_b, hipMemcpyDeviceToHost));
+    QPD_HIP(hipDeviceSynchronize());
+    return QPD_OK;
+}
+
+}  // extern "C"

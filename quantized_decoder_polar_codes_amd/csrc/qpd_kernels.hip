@@ -1,0 +1,620 @@
+// qpd_kernels.hip -- gfx950 kernels for the quantized polar LUT decoders.
+//
+// Work mapping: one 64-lane wavefront per workgroup; a frame
+// owns a group of G = pow2 >= L consecutive lanes, one lane per list path, so
+// a wave decodes 64/G frames at once (8 at L=8, 64 for SC).  Every frame runs
+// the SAME static traversal schedule (host-compiled op list, qpd_capi.hip), so
+// control flow is wave-uniform; only data differs between lanes.
+//
+// List management without the reference's per-fork deep copies
+// (src/SCLLUTDecoder.cpp:135-144): each path keeps, per
+// tree depth, a 4-bit pointer to the lane whose scratch slot holds its data
+// (Balatsoukas-Stimming pointer memory).  A path always writes its own slot;
+// a fork copies two 64-bit pointer words from the parent lane instead of
+// ~450 KB of state.  Path metrics are fp64, accumulated in exactly the
+// reference's order (hazard H5); survivor selection reproduces libstdc++
+// std::sort tie order (H1) -- insertion sort (stable) for 2L <= 16 via exact
+// ranks, full introsort replay (stl_sort.hpp) for the R1 argsort.
+//
+// Per-lane state lives in a per-wave scratch slab laid out [row][64 lanes]
+// (one dword per lane per row), so a row access by the wave is one fully
+// coalesced 256-B transaction; cross-lane reads stay inside that line.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "stl_sort.hpp"
+
+namespace qpd {
+
+enum OpType : int32_t {
+    OP_F = 0,       // left child symbols  (f LUT), depth d -> d+1
+    OP_G = 1,       // right child symbols (g LUT), depth d -> d+1
+    OP_LEAF_L = 2,  // left leaf 2*node of a depth n-1 node (f LUT at j=0)
+    OP_LEAF_R = 3,  // right leaf 2*node+1                  (g LUT at j=0)
+    OP_COMB = 4,    // partial-sum combine u(), utils.cpp:62-67
+    OP_R0 = 5,
+    OP_R1 = 6,
+    OP_REP = 7,
+    OP_SPC = 8
+};
+
+struct Op {
+    int32_t type, d, node, aux;  // aux: frozen flag for leaves
+};
+
+constexpr int kMaxDepth = 16;  // N <= 65536
+constexpr int kMaxL = 8;       // 2L <= 16: libstdc++ sorts by insertion (stable)
+constexpr int kMaxM = kMaxL - 1;
+
+enum Kind : int32_t { K_SC_FLOAT = 0, K_SC_LUT = 1, K_SCL_LUT = 2, K_FASTSC_LUT = 3, K_FASTSCL_LUT = 4 };
+
+struct DevPlan {
+    int32_t N, n, K, L, v, gs, fpw, nops;
+    int32_t f_step, g_step, max_r1;
+    int32_t rows_per_wave;
+    // scratch row offsets: S[d] (symbols of the active node at depth d, bytes),
+    // U[d] (partial sums of the finished left child at depth d, bits),
+    // R (right-chain partial sums, own lane), H (R1 hard decisions),
+    // I / Kd (R1 argsort index / key arrays).
+    int32_t So[kMaxDepth + 1], Uo[kMaxDepth + 1], Ro, Ho, Io, Ko;
+    const uint8_t *lut_f;
+    const int32_t *f_base;
+    const uint8_t *lut_g;
+    const int32_t *g_base;
+    const double *vcl;
+    const Op *ops;
+    const int32_t *info_pos;
+    uint32_t *scratch;
+    int32_t *err;
+};
+
+// ---------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t *row_ptr(uint32_t *wsc, int r) { return wsc + (size_t)r * 64; }
+
+__device__ __forceinline__ int ptr_get(uint64_t p, int d) { return (int)((p >> (4 * d)) & 15u); }
+
+__device__ __forceinline__ uint64_t ptr_set(uint64_t p, int d, int lane_in_group) {
+    const uint64_t m = 15ull << (4 * d);
+    return (p & ~m) | ((uint64_t)lane_in_group << (4 * d));
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t x, int src) {
+    uint32_t lo = __shfl((uint32_t)x, src);
+    uint32_t hi = __shfl((uint32_t)(x >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ double shfld(double x, int src) { return __shfl(x, src); }
+
+__device__ __forceinline__ void wave_sync() { __syncthreads(); }  // 64-thread block: one wave
+
+__device__ __forceinline__ double vcl_at(const DevPlan &P, int row, int pos, int sym) {
+    return P.vcl[((size_t)row * P.N + pos) * P.v + sym];
+}
+
+// Channel symbol read with range check (the reference has none: UB there).
+__device__ __forceinline__ int in_sym(const DevPlan &P, const int32_t *y, int e) {
+    int s = y[e];
+    if ((unsigned)s >= (unsigned)P.v) {
+        atomicOr(P.err, 1);
+        s = 0;
+    }
+    return s;
+}
+
+// Symbol e of the active node at depth d, for the path whose slot is `src`.
+__device__ __forceinline__ int node_sym(const DevPlan &P, uint32_t *wsc, const int32_t *y, int d, int src, int e) {
+    if (d == 0) return in_sym(P, y, e);
+    uint32_t w = row_ptr(wsc, P.So[d] + (e >> 2))[src];
+    return (int)((w >> (8 * (e & 3))) & 255u);
+}
+
+// ---------------------------------------------------------------------------
+// Survivor selection: keep the L best of 2L candidates {keep_j = c_j,
+// flip_j = c_{j+L}} exactly as std::sort(index, key<) + take L (mink,
+// src/SCLLUTDecoder.cpp:8-21).  For 2L <= 16 libstdc++ runs a stable
+// insertion sort, i.e. order by (key, candidate index); rank each candidate by
+// counting the candidates before it, then invert the ranks through LDS.
+// ---------------------------------------------------------------------------
+struct Sel {
+    int parent;  // lane-in-group of the surviving candidate's path
+    bool upper;  // candidate came from the second half (flip / penalty branch)
+};
+
+__device__ __forceinline__ Sel select_survivors(double kk, double kf, int gl, int gbase, int L, int *sel) {
+    int rk = 0, rf = 0;
+    for (int j = 0; j < L; ++j) {
+        const double ok = shfld(kk, gbase + j);
+        const double of = shfld(kf, gbase + j);
+        rk += (ok < kk) || (ok == kk && j < gl);
+        rk += (of < kk);
+        rf += (ok <= kf);
+        rf += (of < kf) || (of == kf && j < gl);
+    }
+    if (gl < L) {
+        if (rk < L) sel[gbase + rk] = gl;
+        if (rf < L) sel[gbase + rf] = gl + L;
+    }
+    wave_sync();
+    int c = (gl < L) ? sel[gbase + gl] : gl;
+    wave_sync();
+    Sel s;
+    s.upper = c >= L;
+    s.parent = s.upper ? c - L : c;
+    return s;
+}
+
+// Write the finished node's partial sums (nbits bits, in `words`) either to the
+// path's own U[d] slot (left child) or to the own R chain (right child / root).
+__device__ __forceinline__ void store_node_word(const DevPlan &P, uint32_t *wsc, int d, bool to_r, int w,
+                                                uint32_t word, int lane) {
+    if (to_r)
+        row_ptr(wsc, P.Ro + w)[lane] = word;
+    else
+        row_ptr(wsc, P.Uo[d] + w)[lane] = word;
+}
+
+// Per-lane argsort arrays for the R1 node (stl_sort.hpp Seq interface).
+struct LaneSortSeq {
+    uint32_t *wsc;
+    int io, ko, lane;
+    __device__ int get(int p) { return (int)row_ptr(wsc, io + p)[lane]; }
+    __device__ void set(int p, int e) { row_ptr(wsc, io + p)[lane] = (uint32_t)e; }
+    __device__ double key(int e) { return ((double *)row_ptr(wsc, ko + 2 * e))[lane]; }
+    __device__ bool less(int a, int b) { return key(a) < key(b); }
+};
+
+// ---------------------------------------------------------------------------
+// LUT decoders (SC-LUT, SCL-LUT, FastSC-LUT, FastSCL-LUT)
+// ---------------------------------------------------------------------------
+template <int KIND>
+__global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t *__restrict__ in, int64_t B,
+                                                        uint8_t *__restrict__ out) {
+    constexpr bool kList = (KIND == K_SCL_LUT || KIND == K_FASTSCL_LUT);
+    __shared__ int sel[64];
+    const int lane = threadIdx.x;
+    const int gs = P.gs;
+    const int gl = lane & (gs - 1);
+    const int gbase = lane & ~(gs - 1);
+    const int L = kList ? P.L : 1;
+    const int N = P.N, n = P.n, v = P.v;
+    const int vv = v * v;
+    uint32_t *wsc = P.scratch + (size_t)blockIdx.x * P.rows_per_wave * 64;
+    const int64_t ngroups = (B + P.fpw - 1) / P.fpw;
+    const double kInf = __builtin_huge_val();
+
+    uint64_t self = 0;
+    for (int d = 0; d < kMaxDepth; ++d) self |= (uint64_t)gl << (4 * d);
+
+    for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+        int64_t frame = grp * P.fpw + lane / gs;
+        const bool frame_ok = frame < B;
+        if (!frame_ok) frame = B - 1;
+        const int32_t *y = in + frame * (int64_t)N;
+        double pm = (gl == 0) ? 0.0 : kInf;
+        uint64_t ps = self, pu = self;
+
+        for (int oi = 0; oi < P.nops; ++oi) {
+            const Op op = P.ops[oi];
+            const int d = op.d, node = op.node;
+            const int posi = (1 << d) + node - 1;
+            switch (op.type) {
+                case OP_F:
+                case OP_G: {
+                    const bool isg = op.type == OP_G;
+                    const int ctemp = N >> (d + 1);
+                    const int src = gbase + ptr_get(ps, d);
+                    const int usrc = gbase + ptr_get(pu, d + 1);
+                    const uint8_t *T = isg ? P.lut_g : P.lut_f;
+                    const int tsz = isg ? 2 * vv : vv;
+                    const int tb = isg ? P.g_base[posi] : P.f_base[posi];
+                    const int ts = isg ? P.g_step : P.f_step;
+                    const int nw = (ctemp + 3) >> 2;
+                    for (int w = 0; w < nw; ++w) {
+                        uint32_t ub = 0;
+                        if (isg) ub = row_ptr(wsc, P.Uo[d + 1] + ((4 * w) >> 5))[usrc] >> ((4 * w) & 31);
+                        uint32_t res = 0;
+                        const int ne = ctemp < 4 ? ctemp : 4;
+                        for (int i = 0; i < ne; ++i) {
+                            const int e = 4 * w + i;
+                            const int a = node_sym(P, wsc, y, d, src, e);
+                            const int b = node_sym(P, wsc, y, d, src, e + ctemp);
+                            const int u = (ub >> i) & 1;
+                            const size_t t = (size_t)(tb + e * ts);
+                            const uint32_t val = T[t * tsz + u * vv + a * v + b];
+                            res |= val << (8 * i);
+                        }
+                        row_ptr(wsc, P.So[d + 1] + w)[lane] = res;
+                    }
+                    ps = ptr_set(ps, d + 1, gl);
+                    break;
+                }
+                case OP_LEAF_L:
+                case OP_LEAF_R: {
+                    const bool right = op.type == OP_LEAF_R;
+                    const int k = 2 * node + (right ? 1 : 0);
+                    const bool frozen = op.aux != 0;
+                    const int src = gbase + ptr_get(ps, d);
+                    uint32_t dec = 0;
+                    if (!kList && frozen) {
+                        dec = 0;  // SCLUTDecoder.cpp:60-61: frozen leaves skip the LUT
+                    } else {
+                        const int a = node_sym(P, wsc, y, d, src, 0);
+                        const int b = node_sym(P, wsc, y, d, src, 1);
+                        int s;
+                        if (right) {
+                            const int u = row_ptr(wsc, P.Uo[n])[gbase + ptr_get(pu, n)] & 1;
+                            s = P.lut_g[(size_t)P.g_base[posi] * 2 * vv + u * vv + a * v + b];
+                        } else {
+                            s = P.lut_f[(size_t)P.f_base[posi] * vv + a * v + b];
+                        }
+                        const double dm = vcl_at(P, n - 1, k, s);  // H3: row n-1
+                        if (!kList) {
+                            dec = dm <= 0;  // H4: SC family `<= 0`
+                        } else if (frozen) {
+                            pm += fabs(dm) * (double)(dm < 0);  // :100-104
+                        } else {
+                            const double kf = pm + fabs(dm);
+                            const Sel sl = select_survivors(pm, kf, gl, gbase, L, sel);
+                            const int p = gbase + sl.parent;
+                            const uint32_t hd = dm < 0;  // H4: SCL family `< 0`
+                            dec = (uint32_t)__shfl((int)hd, p) ^ (sl.upper ? 1u : 0u);
+                            pm = sl.upper ? shfld(kf, p) : shfld(pm, p);
+                            ps = shfl64(ps, p);
+                            pu = shfl64(pu, p);
+                        }
+                    }
+                    if (right) {
+                        row_ptr(wsc, P.Ro)[lane] = dec;
+                    } else {
+                        row_ptr(wsc, P.Uo[n])[lane] = dec;
+                        pu = ptr_set(pu, n, gl);
+                    }
+                    break;
+                }
+                case OP_COMB: {
+                    const int ctemp = N >> (d + 1);
+                    const int usrc = gbase + ptr_get(pu, d + 1);
+                    const bool to_r = (d == 0) || (node & 1);
+                    if (ctemp < 32) {
+                        const uint32_t m = (1u << ctemp) - 1u;
+                        const uint32_t ul = row_ptr(wsc, P.Uo[d + 1])[usrc] & m;
+                        const uint32_t r = row_ptr(wsc, P.Ro)[lane] & m;
+                        store_node_word(P, wsc, d, to_r, 0, (ul ^ r) | (r << ctemp), lane);
+                    } else {
+                        const int cw = ctemp >> 5;
+                        for (int w = 0; w < cw; ++w) {
+                            const uint32_t ul = row_ptr(wsc, P.Uo[d + 1] + w)[usrc];
+                            const uint32_t r = row_ptr(wsc, P.Ro + w)[lane];
+                            store_node_word(P, wsc, d, to_r, cw + w, r, lane);
+                            store_node_word(P, wsc, d, to_r, w, ul ^ r, lane);
+                        }
+                    }
+                    if (!to_r) pu = ptr_set(pu, d, gl);
+                    break;
+                }
+                default: {  // special nodes, FastSCLUT.cpp:46-107 / FastSCLLUTDecoder.cpp:82-213
+                    const int temp = N >> d;
+                    const int src = gbase + ptr_get(ps, d);
+                    const bool to_r = (node & 1);
+                    const int base_pos = temp * node;
+                    const int nwo = (temp + 31) >> 5;
+                    if (op.type == OP_R0) {
+                        if (kList) {
+                            for (int j = 0; j < temp; ++j) {
+                                const double l = vcl_at(P, d - 1, base_pos + j, node_sym(P, wsc, y, d, src, j));
+                                pm += (double)(float)(l < 0) * fabs(l);
+                            }
+                        }
+                        for (int w = 0; w < nwo; ++w) store_node_word(P, wsc, d, to_r, w, 0u, lane);
+                    } else if (op.type == OP_REP) {
+                        uint32_t fill = 0;
+                        if (!kList) {
+                            double S = 0;
+                            for (int j = 0; j < temp; ++j) S += vcl_at(P, d - 1, base_pos + j, node_sym(P, wsc, y, d, src, j));
+                            fill = S <= 0 ? 0xffffffffu : 0u;
+                        } else {
+                            double kk = pm, kf = pm;
+                            for (int j = 0; j < temp; ++j) {
+                                const double l = vcl_at(P, d - 1, base_pos + j, node_sym(P, wsc, y, d, src, j));
+                                kk += (double)(l < 0) * fabs(l);
+                                kf += (double)(l >= 0) * fabs(l);
+                            }
+                            const Sel sl = select_survivors(kk, kf, gl, gbase, L, sel);
+                            const int p = gbase + sl.parent;
+                            pm = sl.upper ? shfld(kf, p) : shfld(kk, p);
+                            ps = shfl64(ps, p);
+                            pu = shfl64(pu, p);
+                            fill = sl.upper ? 0xffffffffu : 0u;
+                        }
+                        const uint32_t m = temp < 32 ? ((1u << temp) - 1u) : 0xffffffffu;
+                        for (int w = 0; w < nwo; ++w) store_node_word(P, wsc, d, to_r, w, fill & m, lane);
+                    } else if (op.type == OP_SPC) {  // FastSC only
+                        uint32_t parity = 0;
+                        double best = 0;
+                        int bi = 0;
+                        for (int w = 0; w < nwo; ++w) {
+                            uint32_t word = 0;
+                            for (int i = 0; i < 32 && 32 * w + i < temp; ++i) {
+                                const int j = 32 * w + i;
+                                const double l = vcl_at(P, d - 1, base_pos + j, node_sym(P, wsc, y, d, src, j));
+                                const uint32_t h = l <= 0;
+                                word |= h << i;
+                                parity ^= h;
+                                const double a = fabs(l);
+                                if (j == 0 || a < best) {  // first minimum (H6)
+                                    best = a;
+                                    bi = j;
+                                }
+                            }
+                            store_node_word(P, wsc, d, to_r, w, word, lane);
+                        }
+                        if (parity) {
+                            uint32_t *pw = to_r ? &row_ptr(wsc, P.Ro + (bi >> 5))[lane]
+                                                : &row_ptr(wsc, P.Uo[d] + (bi >> 5))[lane];
+                            *pw ^= 1u << (bi & 31);
+                        }
+                    } else if (!kList) {  // OP_R1, FastSC: `<= 0`
+                        for (int w = 0; w < nwo; ++w) {
+                            uint32_t word = 0;
+                            for (int i = 0; i < 32 && 32 * w + i < temp; ++i) {
+                                const int j = 32 * w + i;
+                                const double l = vcl_at(P, d - 1, base_pos + j, node_sym(P, wsc, y, d, src, j));
+                                word |= (uint32_t)(l <= 0) << i;
+                            }
+                            store_node_word(P, wsc, d, to_r, w, word, lane);
+                        }
+                    } else if constexpr (KIND == K_FASTSCL_LUT) {  // OP_R1, FastSCL: FastSCLLUTDecoder.cpp:99-166
+                        const int m = (L - 1) < temp ? (L - 1) : temp;
+                        // hard decisions (`< 0`) to own H rows, magnitudes to own key rows
+                        for (int w = 0; w < nwo; ++w) {
+                            uint32_t word = 0;
+                            for (int i = 0; i < 32 && 32 * w + i < temp; ++i) {
+                                const int j = 32 * w + i;
+                                const double l = vcl_at(P, d - 1, base_pos + j, node_sym(P, wsc, y, d, src, j));
+                                word |= (uint32_t)(l < 0) << i;
+                                ((double *)row_ptr(wsc, P.Ko + 2 * j))[lane] = fabs(l);
+                            }
+                            row_ptr(wsc, P.Ho + w)[lane] = word;
+                        }
+                        // first m entries of argsort(|l|) (argsort :7-17, H1)
+                        int ord[kMaxM];
+                        double ms[kMaxM];
+                        int flip[kMaxM];
+#pragma unroll
+                        for (int q = 0; q < kMaxM; ++q) {
+                            ord[q] = 0;
+                            ms[q] = 0;
+                            flip[q] = -1;
+                        }
+                        LaneSortSeq seq{wsc, P.Io, P.Ko, lane};
+                        if (temp <= stl::kThreshold) {
+                            // insertion sort is stable: order by (|l|, index)
+                            uint32_t taken = 0;
+#pragma unroll
+                            for (int q = 0; q < kMaxM; ++q) {
+                                if (q < m) {
+                                    int bj = -1;
+                                    double bk = 0;
+                                    for (int j = 0; j < temp; ++j) {
+                                        if (taken & (1u << j)) continue;
+                                        const double kj = seq.key(j);
+                                        if (bj < 0 || kj < bk) {
+                                            bj = j;
+                                            bk = kj;
+                                        }
+                                    }
+                                    taken |= 1u << bj;
+                                    ord[q] = bj;
+                                    ms[q] = bk;
+                                }
+                            }
+                        } else {
+                            for (int p = 0; p < temp; ++p) seq.set(p, p);
+                            stl::sort(seq, 0, temp);
+#pragma unroll
+                            for (int q = 0; q < kMaxM; ++q) {
+                                if (q < m) {
+                                    ord[q] = seq.get(q);
+                                    ms[q] = seq.key(ord[q]);
+                                }
+                            }
+                        }
+                        wave_sync();  // H rows visible to the other lanes of the group
+                        int origin = gl;
+#pragma unroll
+                        for (int layer = 0; layer < kMaxM; ++layer) {
+                            if (layer < m) {
+                                const double kf = pm + ms[layer];
+                                const Sel sl = select_survivors(pm, kf, gl, gbase, L, sel);
+                                const int p = gbase + sl.parent;
+                                const int pos_old = ord[layer];  // H2: own pre-permutation order
+                                pm = sl.upper ? shfld(kf, p) : shfld(pm, p);
+                                ps = shfl64(ps, p);
+                                pu = shfl64(pu, p);
+                                origin = __shfl(origin, p);
+#pragma unroll
+                                for (int q = 0; q < kMaxM; ++q) {
+                                    ord[q] = __shfl(ord[q], p);
+                                    ms[q] = shfld(ms[q], p);
+                                    if (q < layer) flip[q] = __shfl(flip[q], p);
+                                }
+                                flip[layer] = sl.upper ? pos_old : -1;
+                            }
+                        }
+                        for (int w = 0; w < nwo; ++w) {
+                            uint32_t word = row_ptr(wsc, P.Ho + w)[gbase + origin];
+#pragma unroll
+                            for (int q = 0; q < kMaxM; ++q)
+                                if (q < m && flip[q] >= 0 && (flip[q] >> 5) == w) word ^= 1u << (flip[q] & 31);
+                            if (temp < 32) word &= (1u << temp) - 1u;
+                            store_node_word(P, wsc, d, to_r, w, word, lane);
+                        }
+                    }
+                    if (!to_r) pu = ptr_set(pu, d, gl);
+                    break;
+                }
+            }
+            wave_sync();  // scratch writes of this op visible to the whole wave
+        }
+
+        // Root partial sums (N bits) are in the own R rows.  u = x F^{(x)n}
+        // (re-encoding, FastSCLUT.cpp:186-198; for SC/SCL this reproduces the
+        // leaf decisions the reference reads directly, SCLUTDecoder.cpp:116-123).
+        const int nwr = (N + 31) >> 5;
+        for (int w = 0; w < nwr; ++w) {
+            uint32_t x = row_ptr(wsc, P.Ro + w)[lane];
+            if (N < 32) x &= (1u << N) - 1u;
+            x ^= (x >> 1) & 0x55555555u;
+            x ^= (x >> 2) & 0x33333333u;
+            x ^= (x >> 4) & 0x0f0f0f0fu;
+            x ^= (x >> 8) & 0x00ff00ffu;
+            x ^= (x >> 16) & 0x0000ffffu;
+            row_ptr(wsc, P.Ro + w)[lane] = x;
+        }
+        for (int mw = 1; mw < nwr; mw *= 2)
+            for (int i = 0; i < nwr; i += 2 * mw)
+                for (int j = 0; j < mw; ++j) {
+                    uint32_t *a = &row_ptr(wsc, P.Ro + i + j)[lane];
+                    *a ^= row_ptr(wsc, P.Ro + i + mw + j)[lane];
+                }
+        wave_sync();
+        // best path: first minimum of the path metrics (H6, SCLLUTDecoder.cpp:244)
+        int best = 0;
+        if (kList) {
+            double bpm = shfld(pm, gbase);
+            for (int j = 1; j < L; ++j) {
+                const double pj = shfld(pm, gbase + j);
+                if (pj < bpm) {
+                    bpm = pj;
+                    best = j;
+                }
+            }
+        }
+        if (frame_ok) {
+            const uint32_t *rb = row_ptr(wsc, P.Ro);
+            for (int t = gl; t < P.K; t += gs) {
+                const int pos = P.info_pos[t];
+                out[frame * P.K + t] = (uint8_t)((rb[(size_t)(pos >> 5) * 64 + gbase + best] >> (pos & 31)) & 1u);
+            }
+        }
+        wave_sync();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Float SC (min-sum on fp64 LLRs), SCDecoder.cpp:14-89; one lane per frame.
+// Scratch: stage d (1..n) fp64 rows at So[d] (2 dword rows per element),
+// U/R bit rows as in the LUT kernel.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int sgn(double x) { return x < 0 ? -1 : (x > 0); }
+__device__ __forceinline__ double std_min(double a, double b) { return (b < a) ? b : a; }
+
+__global__ __launch_bounds__(64) void sc_float_kernel(DevPlan P, const double *__restrict__ in, int64_t B,
+                                                      uint8_t *__restrict__ out) {
+    const int lane = threadIdx.x;
+    const int N = P.N, n = P.n;
+    uint32_t *wsc = P.scratch + (size_t)blockIdx.x * P.rows_per_wave * 64;
+    const int64_t ngroups = (B + 63) / 64;
+    for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+        int64_t frame = grp * 64 + lane;
+        const bool frame_ok = frame < B;
+        if (!frame_ok) frame = B - 1;
+        const double *y = in + frame * (int64_t)N;
+        auto alpha = [&](int d, int e) -> double {
+            if (d == 0) return y[e];
+            return ((double *)row_ptr(wsc, P.So[d] + 2 * e))[lane];
+        };
+        auto set_alpha = [&](int d, int e, double x) { ((double *)row_ptr(wsc, P.So[d] + 2 * e))[lane] = x; };
+        for (int oi = 0; oi < P.nops; ++oi) {
+            const Op op = P.ops[oi];
+            const int d = op.d, node = op.node;
+            switch (op.type) {
+                case OP_F:
+                case OP_G: {
+                    const int ctemp = N >> (d + 1);
+                    for (int j = 0; j < ctemp; ++j) {
+                        const double a = alpha(d, j), b = alpha(d, j + ctemp);
+                        double r;
+                        if (op.type == OP_F) {
+                            r = (double)(sgn(a) * sgn(b)) * std_min(fabs(a), fabs(b));
+                        } else {
+                            const int u = (row_ptr(wsc, P.Uo[d + 1] + (j >> 5))[lane] >> (j & 31)) & 1;
+                            r = (double)(1 - 2 * u) * a + b;
+                        }
+                        set_alpha(d + 1, j, r);
+                    }
+                    break;
+                }
+                case OP_LEAF_L:
+                case OP_LEAF_R: {
+                    const bool right = op.type == OP_LEAF_R;
+                    const double a = alpha(d, 0), b = alpha(d, 1);
+                    double l;
+                    if (right) {
+                        const int u = row_ptr(wsc, P.Uo[n])[lane] & 1;
+                        l = (double)(1 - 2 * u) * a + b;
+                    } else {
+                        l = (double)(sgn(a) * sgn(b)) * std_min(fabs(a), fabs(b));
+                    }
+                    const uint32_t dec = op.aux ? 0u : (uint32_t)(l <= 0);
+                    if (right)
+                        row_ptr(wsc, P.Ro)[lane] = dec;
+                    else
+                        row_ptr(wsc, P.Uo[n])[lane] = dec;
+                    break;
+                }
+                case OP_COMB: {
+                    const int ctemp = N >> (d + 1);
+                    const bool to_r = (d == 0) || (node & 1);
+                    if (ctemp < 32) {
+                        const uint32_t m = (1u << ctemp) - 1u;
+                        const uint32_t ul = row_ptr(wsc, P.Uo[d + 1])[lane] & m;
+                        const uint32_t r = row_ptr(wsc, P.Ro)[lane] & m;
+                        store_node_word(P, wsc, d, to_r, 0, (ul ^ r) | (r << ctemp), lane);
+                    } else {
+                        const int cw = ctemp >> 5;
+                        for (int w = 0; w < cw; ++w) {
+                            const uint32_t ul = row_ptr(wsc, P.Uo[d + 1] + w)[lane];
+                            const uint32_t r = row_ptr(wsc, P.Ro + w)[lane];
+                            store_node_word(P, wsc, d, to_r, cw + w, r, lane);
+                            store_node_word(P, wsc, d, to_r, w, ul ^ r, lane);
+                        }
+                    }
+                    break;
+                }
+                default:
+                    break;
+            }
+        }
+        const int nwr = (N + 31) >> 5;
+        for (int w = 0; w < nwr; ++w) {
+            uint32_t x = row_ptr(wsc, P.Ro + w)[lane];
+            if (N < 32) x &= (1u << N) - 1u;
+            x ^= (x >> 1) & 0x55555555u;
+            x ^= (x >> 2) & 0x33333333u;
+            x ^= (x >> 4) & 0x0f0f0f0fu;
+            x ^= (x >> 8) & 0x00ff00ffu;
+            x ^= (x >> 16) & 0x0000ffffu;
+            row_ptr(wsc, P.Ro + w)[lane] = x;
+        }
+        for (int mw = 1; mw < nwr; mw *= 2)
+            for (int i = 0; i < nwr; i += 2 * mw)
+                for (int j = 0; j < mw; ++j) {
+                    uint32_t *a = &row_ptr(wsc, P.Ro + i + j)[lane];
+                    *a ^= row_ptr(wsc, P.Ro + i + mw + j)[lane];
+                }
+        if (frame_ok) {
+            const uint32_t *rb = row_ptr(wsc, P.Ro);
+            for (int t = 0; t < P.K; ++t) {
+                const int pos = P.info_pos[t];
+                out[frame * P.K + t] = (uint8_t)((rb[(size_t)(pos >> 5) * 64 + lane] >> (pos & 31)) & 1u);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace qpd

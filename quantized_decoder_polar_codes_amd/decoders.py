@@ -1,0 +1,210 @@
+"""Host-side mirror of the reference's pybind11 decoder classes.
+
+Same class names, positional order, keyword names and ``decode`` argument as
+the reference (py_interface/py_SCLUTDecoder.cpp:11-14, py_SCLLUTDecoder.cpp:12-15,
+py_FastSCLUTDecoder.cpp:12-15, py_FastSCLLUTDecoder.cpp:13-16,
+py_SCDecoder.cpp:10-12): ``decode`` takes one frame and returns a new
+``numpy.ndarray`` of dtype uint8 and length K.  Every decode runs on the GPU
+through libqpd.so; there is no CPU path.
+
+Additions (not in the reference): ``decode_batch(x[B, N])`` for throughput
+(numpy in -> numpy out; a torch CUDA tensor in -> torch CUDA tensor out,
+asynchronous on torch's current stream), and validation with ``ValueError``
+where the reference has undefined behaviour.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .lut import PackedLUT, pack_luts
+
+__all__ = ["SCDecoder", "SCLUTDecoder", "SCLLUTDecoder", "FastSCLUTDecoder", "FastSCLLUTDecoder"]
+
+
+def _as_i32(x) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(x).astype(np.int32))
+
+
+def _ptr(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def _torch():
+    try:
+        import torch  # noqa: F401
+
+        return torch
+    except Exception:  # pragma: no cover - torch is part of the image
+        return None
+
+
+class _DecoderBase:
+    _kind: int = -1
+    _float_input = False
+
+    def __init__(self, N, K, L, frozen_bits, message_bits, node_type, packed: PackedLUT | None, device=None,
+                 max_waves: int = 0):
+        self.N = int(N)
+        self.K = int(K)
+        self.L = int(L)
+        frozen = _as_i32(frozen_bits).reshape(-1)
+        if frozen.size != self.N:
+            raise ValueError(f"frozen_bits must have N={self.N} entries, got {frozen.size}")
+        self.frozen_bits = frozen
+        # message_bits is stored but never read by the reference
+        self.message_bits = np.asarray(message_bits)
+        self.node_type = None if node_type is None else _as_i32(node_type).reshape(-1)
+        if self.node_type is not None and self.node_type.size != 2 * self.N - 1:
+            raise ValueError(f"node_type must have 2N-1={2 * self.N - 1} entries, got {self.node_type.size}")
+        self.packed = packed
+        lib = _lib.load()
+        cfg = _lib.QpdConfig()
+        cfg.kind = self._kind
+        cfg.N, cfg.K, cfg.L = self.N, self.K, self.L
+        cfg.frozen_bits = _ptr(self.frozen_bits)
+        cfg.node_type = _ptr(self.node_type)
+        if packed is not None:
+            if packed.N != self.N:
+                raise ValueError(f"tables are for N={packed.N}, decoder N={self.N}")
+            cfg.v = packed.v
+            cfg.lut_f, cfg.lut_f_count = _ptr(packed.lut_f), packed.lut_f.shape[0]
+            cfg.f_base, cfg.f_step = _ptr(packed.f_base), packed.f_step
+            cfg.lut_g, cfg.lut_g_count = _ptr(packed.lut_g), packed.lut_g.shape[0]
+            cfg.g_base, cfg.g_step = _ptr(packed.g_base), packed.g_step
+            cfg.vcl, cfg.vcl_rows = _ptr(packed.vcl), packed.vcl_rows
+        if device is None:
+            torch = _torch()
+            device = torch.cuda.current_device() if torch is not None and torch.cuda.is_available() else -1
+        self.device = int(device)
+        cfg.device = self.device
+        cfg.max_waves = int(max_waves)
+        h = ctypes.c_void_p()
+        _lib.check(lib.qpd_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.load().qpd_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    # -- introspection ---------------------------------------------------------
+    def info(self) -> dict:
+        inf = _lib.QpdInfo()
+        _lib.check(_lib.load().qpd_get_info(self._h, ctypes.byref(inf)))
+        return {k: getattr(inf, k) for k, _ in inf._fields_}
+
+    # -- decoding --------------------------------------------------------------
+    def _frame(self, x) -> np.ndarray:
+        a = np.asarray(x)
+        a = a.astype(np.float64 if self._float_input else np.int32).reshape(-1)
+        if a.size < self.N:
+            raise ValueError(f"decode expects N={self.N} values, got {a.size}")
+        # the reference reads the first N values of the buffer (shape (N,) or (1, N))
+        return np.ascontiguousarray(a[: self.N])
+
+    def decode_batch(self, x):
+        """Decode B frames.  numpy [B, N] -> numpy uint8 [B, K] (synchronous);
+        torch CUDA tensor [B, N] -> torch CUDA uint8 [B, K] on the current stream."""
+        torch = _torch()
+        lib = _lib.load()
+        if torch is not None and isinstance(x, torch.Tensor) and x.is_cuda:
+            want = torch.float64 if self._float_input else torch.int32
+            xs = x.reshape(-1, self.N).to(want).contiguous()
+            B = xs.shape[0]
+            out = torch.empty((B, self.K), dtype=torch.uint8, device=xs.device)
+            stream = torch.cuda.current_stream(xs.device).cuda_stream
+            fn = lib.qpd_decode_f64 if self._float_input else lib.qpd_decode
+            _lib.check(fn(self._h, ctypes.c_void_p(xs.data_ptr()), B, ctypes.c_void_p(out.data_ptr()),
+                          ctypes.c_void_p(stream)))
+            return out
+        if torch is not None and isinstance(x, torch.Tensor):
+            x = x.numpy()
+        a = np.asarray(x)
+        a = np.ascontiguousarray(a.astype(np.float64 if self._float_input else np.int32).reshape(-1, self.N))
+        B = a.shape[0]
+        out = np.empty((B, self.K), dtype=np.uint8)
+        fn = lib.qpd_decode_f64_host if self._float_input else lib.qpd_decode_host
+        _lib.check(fn(self._h, _ptr(a), B, _ptr(out)))
+        return out
+
+    def _decode_one(self, x) -> np.ndarray:
+        return self.decode_batch(self._frame(x)[None])[0].copy()
+
+
+class _LUTDecoder(_DecoderBase):
+    def decode(self, channel_quantized_symbols):
+        return self._decode_one(channel_quantized_symbols)
+
+
+class SCLUTDecoder(_LUTDecoder):
+    """SC-LUT (SCLUTDecoder.cpp:21-124)."""
+
+    _kind = _lib.QPD_SC_LUT
+
+    def __init__(self, N, K, frozen_bits, message_bits, LUT_f, LUT_g, virtual_channel_llr, **kw):
+        super().__init__(N, K, 1, frozen_bits, message_bits, None, pack_luts(int(N), LUT_f, LUT_g, virtual_channel_llr),
+                         **kw)
+
+
+class SCLLUTDecoder(_LUTDecoder):
+    """SCL-LUT (SCLLUTDecoder.cpp:47-253)."""
+
+    _kind = _lib.QPD_SCL_LUT
+
+    def __init__(self, N, K, L, frozen_bits, message_bits, LUT_f, LUT_g, virtual_channel_llr, **kw):
+        super().__init__(N, K, L, frozen_bits, message_bits, None, pack_luts(int(N), LUT_f, LUT_g, virtual_channel_llr),
+                         **kw)
+
+
+class FastSCLUTDecoder(_DecoderBase):
+    """FastSC-LUT (FastSCLUT.cpp:27-206); note the reference's kwargs LUT_Fs/LUT_Gs
+    and decode(llr) (py_FastSCLUTDecoder.cpp:12-15)."""
+
+    _kind = _lib.QPD_FASTSC_LUT
+
+    def __init__(self, N, K, frozen_bits, message_bits, node_type, LUT_Fs, LUT_Gs, virtual_channel_llr, **kw):
+        super().__init__(N, K, 1, frozen_bits, message_bits, node_type,
+                         pack_luts(int(N), LUT_Fs, LUT_Gs, virtual_channel_llr), **kw)
+
+    def decode(self, llr):
+        return self._decode_one(llr)
+
+
+class FastSCLLUTDecoder(_LUTDecoder):
+    """FastSCL-LUT (FastSCLLUTDecoder.cpp:57-408)."""
+
+    _kind = _lib.QPD_FASTSCL_LUT
+
+    def __init__(self, N, K, L, frozen_bits, message_bits, node_type, LUT_f, LUT_g, virtual_channel_llr, **kw):
+        super().__init__(N, K, L, frozen_bits, message_bits, node_type,
+                         pack_luts(int(N), LUT_f, LUT_g, virtual_channel_llr), **kw)
+
+
+class SCDecoder(_DecoderBase):
+    """Float SC, min-sum on float64 LLRs (SCDecoder.cpp:14-89)."""
+
+    _kind = _lib.QPD_SC_FLOAT
+    _float_input = True
+
+    def __init__(self, N, K, frozen_bits, message_bits, **kw):
+        super().__init__(N, K, 1, frozen_bits, message_bits, None, None, **kw)
+
+    def decode(self, llr):
+        return self._decode_one(llr)
+
+
+def from_packed(kind: str, packed: PackedLUT, K: int, frozen_bits, L: int = 1, node_type=None, **kw):
+    """Build a decoder directly from packed tables (skips the nested-list path)."""
+    cls = {"SC-LUT": SCLUTDecoder, "SCL-LUT": SCLLUTDecoder, "FastSC-LUT": FastSCLUTDecoder,
+           "FastSCL-LUT": FastSCLLUTDecoder}[kind]
+    obj = cls.__new__(cls)
+    _DecoderBase.__init__(obj, packed.N, K, L if kind in ("SCL-LUT", "FastSCL-LUT") else 1, frozen_bits,
+                          1 - np.asarray(frozen_bits), node_type, packed, **kw)
+    return obj

@@ -1,0 +1,126 @@
+"""Generate the golden fixtures in tests/golden/*.npz.
+
+Inputs are produced here (seeded numpy); expected outputs come from the
+REFERENCE decoders compiled from their own sources under /root/reference
+(oracle/build_ref.sh -> oracle/_ref/_refPolarDecoder*.so), called one frame at
+a time through their pybind11 ``decode`` exactly as the reference drivers do
+(mainQuantizedDecoder_LLRDomain.py:178, mainFPDecoder.py:113).  The reference
+ships no fixtures or tests of its own, so these vectors are
+the pin for both the CPU oracle and the GPU path.
+
+Frames follow the reference driver's channel model
+(mainQuantizedDecoder_LLRDomain.py:132-176): message bits, polar encoding
+(restated PolarEnc), BPSK, AWGN at Eb/N0 with sigma = sqrt(1/(2 R Eb/N0)),
+LLR = 2y/sigma^2, then a channel quantizer to `v` symbols.  The channel
+quantizer here is uniform (MinDistortion channel design needs the OpenCV
+quantizer module, which the image lacks); decoder parity does not depend on
+how symbols or tables were designed.
+
+Usage:  python tests/golden/make_golden.py      (needs oracle/_ref built)
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import oracle as O  # noqa: E402
+from quantized_decoder_polar_codes_amd import codes as C  # noqa: E402
+from quantized_decoder_polar_codes_amd import lut as LU  # noqa: E402
+
+
+def awgn_llr(rng, N, K, msgbits, B, ebn0_db):
+    rate = K / N
+    sigma = np.sqrt(1 / (2 * rate * 10 ** (ebn0_db / 10)))
+    msg = rng.integers(0, 2, size=(B, K), dtype=np.uint8)
+    x = C.polar_encode(msg, msgbits, N)
+    y = (1.0 - 2.0 * x) + rng.normal(0, sigma, size=(B, N))
+    return msg, y * 2 / sigma ** 2
+
+
+def uniform_channel_symbols(llr, v, delta):
+    # symbol s <-> quanta (s - (v-1)/2) * delta: nearest quantum, saturating
+    return np.clip(np.rint(llr / delta + (v - 1) / 2.0), 0, v - 1).astype(np.int32)
+
+
+def ref_decode(R, kind, N, K, L, frozen, msgmask, node_type, packed, sym):
+    fs, gs, vcl = LU.unpack_to_reference(packed)
+    fz, mm = frozen.astype(int).tolist(), msgmask.astype(int).tolist()
+    if kind == "SC-LUT":
+        d = R.SCLUTDecoder(N, K, fz, mm, fs, gs, vcl)
+    elif kind == "SCL-LUT":
+        d = R.SCLLUTDecoder(N, K, L, fz, mm, fs, gs, vcl)
+    elif kind == "FastSC-LUT":
+        d = R.FastSCLUTDecoder(N, K, fz, mm, node_type.tolist(), fs, gs, vcl)
+    elif kind == "FastSCL-LUT":
+        d = R.FastSCLLUTDecoder(N, K, L, fz, mm, node_type.tolist(), fs, gs, vcl)
+    else:
+        raise ValueError(kind)
+    return np.stack([d.decode(s.astype(np.int32)) for s in sym]).astype(np.uint8)
+
+
+def make_lut_case(R, name, kind, N, K, L, lut_kind, B, ebn0, seed):
+    rng = np.random.default_rng(seed)
+    _, msgbits, frozen, msgmask = C.construct_pw(N, K)
+    node_type = C.identify_nodes(N, msgbits).astype(np.int32)
+    v, delta = 16, 0.5
+    if lut_kind == "minsum":
+        packed = LU.minsum_uniform_luts(N, v=v, delta=delta)
+    else:
+        packed = LU.random_luts(N, v=v, seed=seed, distinct_mags=4)
+    msg, llr = awgn_llr(rng, N, K, msgbits, B, ebn0)
+    sym = uniform_channel_symbols(llr, v, delta)
+    if lut_kind != "minsum":
+        sym = rng.integers(0, v, size=sym.shape, dtype=np.int32)  # random tables: random symbols
+    t = time.time()
+    out = ref_decode(R, kind, N, K, L, frozen, msgmask, node_type, packed, sym)
+    dt = time.time() - t
+    np.savez_compressed(
+        os.path.join(HERE, name + ".npz"),
+        kind=kind, N=N, K=K, L=L, v=v, lut_kind=lut_kind, ebn0_db=ebn0, seed=seed,
+        frozen=frozen.astype(np.int8), node_type=node_type.astype(np.int8),
+        lut_f=packed.lut_f, f_base=packed.f_base, f_step=packed.f_step,
+        lut_g=packed.lut_g, g_base=packed.g_base, g_step=packed.g_step,
+        vcl=packed.vcl, msg=msg, symbols=sym.astype(np.uint8), expected=out,
+    )
+    errs = (out != msg).any(1).mean() if lut_kind == "minsum" else float("nan")
+    print(f"{name:28s} {kind:12s} N={N} K={K} L={L} B={B} ref {dt:.1f}s  BLER={errs:.3f}")
+
+
+def make_float_case(R, name, N, K, B, ebn0, seed):
+    rng = np.random.default_rng(seed)
+    _, msgbits, frozen, msgmask = C.construct_pw(N, K)
+    msg, llr = awgn_llr(rng, N, K, msgbits, B, ebn0)
+    llr[:3, :5] = 0.0  # exact zeros: `alpha <= 0` and sign(0) = 0 paths
+    d = R.SCDecoder(N, K, frozen.astype(int).tolist(), msgmask.astype(int).tolist())
+    out = np.stack([d.decode(x[None]) for x in llr]).astype(np.uint8)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), kind="SC", N=N, K=K, L=1, ebn0_db=ebn0, seed=seed,
+                        frozen=frozen.astype(np.int8), msg=msg, llr=llr, expected=out)
+    print(f"{name:28s} SC float     N={N} K={K} B={B}  BLER={(out != msg).any(1).mean():.3f}")
+
+
+def main():
+    R = O.reference_module()
+    if R is None:
+        raise SystemExit("oracle/_ref not built (run oracle/build_ref.sh)")
+    make_float_case(R, "sc_float_n128_k32", 128, 32, 400, 2.0, 1)
+    make_lut_case(R, "sclut_n128_k32_minsum", "SC-LUT", 128, 32, 1, "minsum", 2000, 2.0, 2)
+    make_lut_case(R, "sclut_n128_k32_random", "SC-LUT", 128, 32, 1, "random", 1000, 2.0, 3)
+    make_lut_case(R, "scllut_n128_k64_l8_random", "SCL-LUT", 128, 64, 8, "random", 500, 2.0, 4)
+    make_lut_case(R, "fastscllut_n128_k64_l8_random", "FastSCL-LUT", 128, 64, 8, "random", 500, 2.0, 5)
+    make_lut_case(R, "fastsclut_n128_k64_random", "FastSC-LUT", 128, 64, 1, "random", 1000, 2.0, 6)
+    make_lut_case(R, "scllut_n1024_k512_l8_minsum", "SCL-LUT", 1024, 512, 8, "minsum", 200, 2.0, 7)
+    make_lut_case(R, "fastscllut_n1024_k512_l8_minsum", "FastSCL-LUT", 1024, 512, 8, "minsum", 200, 2.0, 8)
+    make_lut_case(R, "fastsclut_n1024_k512_minsum", "FastSC-LUT", 1024, 512, 1, "minsum", 300, 2.0, 9)
+    make_lut_case(R, "sclut_n1024_k512_minsum", "SC-LUT", 1024, 512, 1, "minsum", 300, 2.0, 10)
+
+
+if __name__ == "__main__":
+    main()

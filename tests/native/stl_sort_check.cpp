@@ -1,0 +1,43 @@
+// Host check: qpd::stl::sort (csrc/stl_sort.hpp) == libstdc++ std::sort on
+// index arrays ordered by tie-heavy double keys.  Built and run by
+// tests/test_stl_sort.py.
+#include <algorithm>
+#include <cstdio>
+#include <random>
+#include <vector>
+#include "stl_sort.hpp"
+
+struct VecSeq {
+    std::vector<int> &idx;
+    const std::vector<double> &key;
+    int get(int p) { return idx[p]; }
+    void set(int p, int e) { idx[p] = e; }
+    bool less(int a, int b) { return key[a] < key[b]; }
+};
+
+int main(int argc, char **argv) {
+    long trials = argc > 1 ? atol(argv[1]) : 200000;
+    std::mt19937_64 rng(12345);
+    long bad = 0;
+    for (long t = 0; t < trials; ++t) {
+        int n = 1 + rng() % 300;
+        if (t % 3 == 0) n = 17 + rng() % 48;  // the R1-node sizes of interest
+        int distinct = 1 + rng() % 8;
+        std::vector<double> key(n);
+        for (auto &k : key) k = (double)(rng() % distinct) * 0.5;
+        if (t % 11 == 0)  // organ pipe / sawtooth: drives introsort into heap sort
+            for (int i = 0; i < n; ++i) key[i] = (t % 2) ? (i < n / 2 ? i : n - i) : (double)((i * 7919) % n);
+        if (t % 5 == 0) std::sort(key.begin(), key.end());           // presorted
+        if (t % 7 == 0) std::sort(key.rbegin(), key.rend());         // reversed
+        std::vector<int> a(n), b(n);
+        for (int i = 0; i < n; ++i) a[i] = b[i] = i;
+        std::sort(a.begin(), a.end(), [&](int p, int q) { return key[p] < key[q]; });
+        VecSeq s{b, key};
+        qpd::stl::sort(s, 0, n);
+        if (a != b) {
+            if (++bad < 5) printf("mismatch n=%d distinct=%d\n", n, distinct);
+        }
+    }
+    printf("trials=%ld mismatches=%ld\n", trials, bad);
+    return bad ? 1 : 0;
+}

@@ -1,0 +1,16 @@
+"""csrc/stl_sort.hpp (the device replay of libstdc++ std::sort used for the
+FastSCL-LUT R1 argsort, hazard H1) equals std::sort on tie-heavy inputs,
+including inputs that drive introsort into its heap-sort fallback."""
+import os
+import subprocess
+
+from conftest import ROOT
+
+
+def test_stl_sort_matches_std_sort(tmp_path):
+    exe = tmp_path / "stl_sort_check"
+    subprocess.run(["g++", "-O2", "-std=c++14", "-I", os.path.join(ROOT, "quantized_decoder_polar_codes_amd", "csrc"),
+                    os.path.join(ROOT, "tests", "native", "stl_sort_check.cpp"), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe), "60000"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches=0" in r.stdout
