@@ -92,6 +92,13 @@ def load():
             f"{LIB_PATH} is missing: build it with "
             "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)"
         )
+    # One HIP runtime per process: torch's wheel bundles libamdhip64.so with the
+    # same SONAME as /opt/rocm's.  Loading torch first makes libqpd.so bind to
+    # the runtime torch already uses (device memory and streams are shared).
+    try:
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch is part of the image
+        pass
     L = ctypes.CDLL(LIB_PATH)
     L.qpd_abi_version.restype = ctypes.c_int
     L.qpd_last_error.restype = ctypes.c_char_p

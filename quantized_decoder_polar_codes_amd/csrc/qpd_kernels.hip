@@ -88,6 +88,11 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t x, int src) {
 
 __device__ __forceinline__ double shfld(double x, int src) { return __shfl(x, src); }
 
+// Cross-lane reads (ds_bpermute) see 0 from lanes that are inactive for the
+// instruction, so every shuffle runs with the whole wave active: evaluate both
+// sides first, then select (never `c ? __shfl(a) : __shfl(b)`).
+__device__ __forceinline__ double pick(bool c, double a, double b) { return c ? a : b; }
+
 __device__ __forceinline__ void wave_sync() { __syncthreads(); }  // 64-thread block: one wave
 
 __device__ __forceinline__ double vcl_at(const DevPlan &P, int row, int pos, int sym) {
@@ -261,7 +266,7 @@ __global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t
                             const int p = gbase + sl.parent;
                             const uint32_t hd = dm < 0;  // H4: SCL family `< 0`
                             dec = (uint32_t)__shfl((int)hd, p) ^ (sl.upper ? 1u : 0u);
-                            pm = sl.upper ? shfld(kf, p) : shfld(pm, p);
+                            pm = pick(sl.upper, shfld(kf, p), shfld(pm, p));
                             ps = shfl64(ps, p);
                             pu = shfl64(pu, p);
                         }
@@ -324,7 +329,7 @@ __global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t
                             }
                             const Sel sl = select_survivors(kk, kf, gl, gbase, L, sel);
                             const int p = gbase + sl.parent;
-                            pm = sl.upper ? shfld(kf, p) : shfld(kk, p);
+                            pm = pick(sl.upper, shfld(kf, p), shfld(kk, p));
                             ps = shfl64(ps, p);
                             pu = shfl64(pu, p);
                             fill = sl.upper ? 0xffffffffu : 0u;
@@ -431,7 +436,7 @@ __global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t
                                 const Sel sl = select_survivors(pm, kf, gl, gbase, L, sel);
                                 const int p = gbase + sl.parent;
                                 const int pos_old = ord[layer];  // H2: own pre-permutation order
-                                pm = sl.upper ? shfld(kf, p) : shfld(pm, p);
+                                pm = pick(sl.upper, shfld(kf, p), shfld(pm, p));
                                 ps = shfl64(ps, p);
                                 pu = shfl64(pu, p);
                                 origin = __shfl(origin, p);

@@ -85,6 +85,13 @@ def test_gpu_matches_oracle(N, K, L, tables, kind, qpd, oracle_mod):
     fm, nt = _node_type(N, K)
     B = 24 if N >= 1024 and kind in ("SCL-LUT", "FastSCL-LUT") else 200
     sym = np.random.default_rng(seed).integers(0, 16, size=(B, N), dtype=np.int32)
+    special_root = (kind == "FastSC-LUT" and 0 <= nt[0] <= 3) or (kind == "FastSCL-LUT" and 0 <= nt[0] <= 2)
+    if special_root:  # undefined behaviour in the reference: both sides refuse
+        with pytest.raises(RuntimeError):
+            oracle_mod.decode_lut(kind, p, K, L, fm, sym, node_type=nt)
+        with pytest.raises(ValueError):
+            qpd.from_packed(kind, p, K, fm, L=L, node_type=nt)
+        return
     want = oracle_mod.decode_lut(kind, p, K, L, fm, sym, node_type=nt)
     dec = qpd.from_packed(kind, p, K, fm, L=L, node_type=nt)
     got = dec.decode_batch(sym)
