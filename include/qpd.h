@@ -92,7 +92,12 @@ typedef struct qpd_config {
     int32_t vcl_rows;           /* >= log2(N)                                     */
     int32_t device;             /* HIP device ordinal (-1 = current device)       */
     int32_t max_waves;          /* persistent-grid size cap (0 = default)         */
+    int32_t engine;             /* enum qpd_engine (0 = auto)                     */
 } qpd_config;
+
+/* Kernel selection.  AUTO picks FAST when the tables allow it (one table per
+ * node, v <= 16) and GENERIC otherwise; the env var QPD_ENGINE overrides. */
+enum qpd_engine { QPD_ENGINE_AUTO = 0, QPD_ENGINE_GENERIC = 1, QPD_ENGINE_FAST = 2 };
 
 typedef struct qpd_decoder qpd_decoder;
 
@@ -123,6 +128,9 @@ typedef struct qpd_info {
     int32_t lanes_per_frame;  /* lane stride of one frame (pow2 >= L)        */
     int32_t max_waves;        /* persistent grid cap                         */
     int64_t scratch_bytes_per_wave;
+    int32_t engine;           /* enum qpd_engine actually used               */
+    int32_t lds_bytes_per_wave;
+    int32_t lds_from_depth;   /* fast engine: tree depths >= this live in LDS */
 } qpd_info;
 int qpd_get_info(const qpd_decoder *dec, qpd_info *info);
 

@@ -13,6 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libqpd.so")
 
 QPD_SC_FLOAT, QPD_SC_LUT, QPD_SCL_LUT, QPD_FASTSC_LUT, QPD_FASTSCL_LUT = range(5)
+QPD_ENGINE_AUTO, QPD_ENGINE_GENERIC, QPD_ENGINE_FAST = range(3)
 QPD_OK, QPD_E_INVALID, QPD_E_UNSUPPORTED, QPD_E_DEVICE, QPD_E_INPUT = 0, -1, -2, -3, -4
 
 # Every symbol include/qpd.h declares (tests check the library exports them).
@@ -55,6 +56,7 @@ class QpdConfig(ctypes.Structure):
         ("vcl_rows", _i32),
         ("device", _i32),
         ("max_waves", _i32),
+        ("engine", _i32),
     ]
 
 
@@ -70,6 +72,9 @@ class QpdInfo(ctypes.Structure):
         ("lanes_per_frame", _i32),
         ("max_waves", _i32),
         ("scratch_bytes_per_wave", _i64),
+        ("engine", _i32),
+        ("lds_bytes_per_wave", _i32),
+        ("lds_from_depth", _i32),
     ]
 
 

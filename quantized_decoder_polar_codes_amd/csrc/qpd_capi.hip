@@ -11,7 +11,8 @@
 #include <vector>
 
 #include "qpd.h"
-#include "qpd_kernels.hip"
+#include "qpd_generic.hip"
+#include "qpd_fast.hip"
 
 namespace {
 
@@ -99,7 +100,11 @@ struct qpd_decoder {
     int kind, N, n, K, L, v, device;
     int max_waves;
     int64_t scratch_bytes_per_wave;
+    int engine = QPD_ENGINE_GENERIC;
+    int lds_bytes = 0;
     DevPlan plan{};
+    qpd::FastPlan fplan{};
+    DeviceBuf f_tab, g_tab, fscratch;
     std::vector<Op> ops_host;
     DeviceBuf lut_f, f_base, lut_g, g_base, vcl, ops, info_pos, scratch, err;
     // staging for the host-buffer entry points
@@ -168,6 +173,102 @@ int validate(const qpd_config *c, int *n_out) {
     return QPD_OK;
 }
 
+
+// Fast-engine plan (qpd_fast.hip): nibble-packed per-node tables and the
+// per-depth placement of the path buffers (deep levels in LDS, shallow levels
+// in a global scratch slab), sized to the LDS budget per wave.
+int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
+    qpd::FastPlan &F = d->fplan;
+    const int N = c->N, n = d->n, v = c->v;
+    F.N = N;
+    F.n = n;
+    F.K = c->K;
+    F.L = d->L;
+    F.v = v;
+    F.gs = d->plan.gs;
+    F.fpw = d->plan.fpw;
+    F.nops = (int)s.ops.size();
+    F.max_r1 = s.max_r1;
+    auto srows = [&](int dd) { return std::max(1, (N >> dd) / 8); };
+    auto brows = [&](int dd) { return std::max(1, (N >> dd) / 32); };
+    auto lds_rows = [&](int D) {
+        int r = 0;
+        for (int dd = std::max(D, 1); dd <= n - 1; ++dd) r += srows(dd);
+        for (int dd = std::max(D, 1); dd <= n; ++dd) r += brows(dd);
+        for (int dd = D; dd <= n; ++dd) r += brows(dd);
+        return r;
+    };
+    int budget = 16 * 1024;
+    if (const char *e = getenv("QPD_LDS_BUDGET")) budget = atoi(e);
+    int D = 0;
+    while (D <= n && 256 + lds_rows(D) * 256 > budget) ++D;
+    F.lds_from = D;
+    int rl = 0, rg = 0;
+    for (int dd = 0; dd <= qpd::kMaxDepth; ++dd) F.S_row[dd] = F.U_row[dd] = F.R_row[dd] = 0;
+    for (int dd = 1; dd <= n - 1; ++dd) {
+        int &r = dd >= D ? rl : rg;
+        F.S_row[dd] = r;
+        r += srows(dd);
+    }
+    for (int dd = 1; dd <= n; ++dd) {
+        int &r = dd >= D ? rl : rg;
+        F.U_row[dd] = r;
+        r += brows(dd);
+    }
+    for (int dd = 0; dd <= n; ++dd) {
+        int &r = dd >= D ? rl : rg;
+        F.R_row[dd] = r;
+        r += brows(dd);
+    }
+    F.H_row = F.K_row = F.I_row = rg;
+    if (c->kind == QPD_FASTSCL_LUT && s.max_r1 > 0) {
+        F.H_row = rg;
+        rg += (s.max_r1 + 31) / 32;
+        F.K_row = rg;
+        rg += 2 * s.max_r1;
+        F.I_row = rg;
+        if (s.max_r1 > qpd::stl::kThreshold) rg += s.max_r1;
+    }
+    F.lds_rows = rl;
+    F.glb_rows = std::max(rg, 1);
+    d->lds_bytes = 256 + rl * 256;
+    // nibble-packed tables: entry (u, a, b) of node p at bit 4*(idx&7) of dword idx>>3
+    std::vector<uint32_t> ft((size_t)(N - 1) * 32, 0), gt((size_t)(N - 1) * 64, 0);
+    const size_t vv = (size_t)v * v;
+    for (int p = 0; p < N - 1; ++p) {
+        const uint8_t *tf = c->lut_f + (size_t)c->f_base[p] * vv;
+        const uint8_t *tg = c->lut_g + (size_t)c->g_base[p] * 2 * vv;
+        for (int a = 0; a < v; ++a)
+            for (int b = 0; b < v; ++b) {
+                const int idx = a * 16 + b;
+                ft[(size_t)p * 32 + (idx >> 3)] |= (uint32_t)tf[a * v + b] << (4 * (idx & 7));
+                for (int u = 0; u < 2; ++u) {
+                    const int gi = u * 256 + idx;
+                    gt[(size_t)p * 64 + (gi >> 3)] |= (uint32_t)tg[u * vv + a * v + b] << (4 * (gi & 7));
+                }
+            }
+    }
+    int rc = upload(d->f_tab, ft.data(), ft.size());
+    if (rc) return rc;
+    rc = upload(d->g_tab, gt.data(), gt.size());
+    if (rc) return rc;
+    const int64_t per_wave = (int64_t)F.glb_rows * 64 * 4;
+    int mw = c->max_waves > 0 ? c->max_waves : 256 * 12;
+    mw = (int)std::max<int64_t>(1, std::min<int64_t>(mw, ((int64_t)2 << 30) / per_wave));
+    d->max_waves = mw;
+    d->scratch_bytes_per_wave = per_wave;
+    QPD_HIP(hipMalloc(&d->fscratch.p, (size_t)per_wave * mw));
+    F.f_tab = (const uint32_t *)d->f_tab.p;
+    F.g_tab = (const uint32_t *)d->g_tab.p;
+    F.vcl = (const double *)d->vcl.p;
+    F.ops = (const Op *)d->ops.p;
+    F.info_pos = (const int32_t *)d->info_pos.p;
+    F.scratch = (uint32_t *)d->fscratch.p;
+    F.err = (int32_t *)d->err.p;
+    F.nops = (int)s.ops.size();
+    return QPD_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -197,6 +298,16 @@ int qpd_create(const qpd_config *c, qpd_decoder **out) {
     Schedule s;
     visit(s, c->kind, c->N, n, c->frozen_bits, (c->kind == QPD_FASTSC_LUT || c->kind == QPD_FASTSCL_LUT) ? c->node_type : nullptr, 0, 0);
     d->ops_host = s.ops;
+    {
+        const bool fast_ok = c->kind != QPD_SC_FLOAT && c->f_step == 0 && c->g_step == 0 && c->v <= 16;
+        int want = c->engine;
+        if (const char *e = getenv("QPD_ENGINE")) want = atoi(e);
+        if (want == QPD_ENGINE_FAST && !fast_ok) {
+            delete d;
+            return fail(QPD_E_UNSUPPORTED, "fast engine needs one table per node (f_step = g_step = 0) and v <= 16");
+        }
+        d->engine = (want == QPD_ENGINE_GENERIC || !fast_ok) ? QPD_ENGINE_GENERIC : QPD_ENGINE_FAST;
+    }
 
     DevPlan &P = d->plan;
     P.N = c->N;
@@ -265,7 +376,8 @@ int qpd_create(const qpd_config *c, qpd_decoder **out) {
         QPD_TRY(upload(d->vcl, c->vcl, (size_t)c->vcl_rows * N * c->v));
     }
     {
-        hipError_t e = hipMalloc(&d->scratch.p, (size_t)d->scratch_bytes_per_wave * mw);
+        hipError_t e = hipSuccess;
+        if (d->engine == QPD_ENGINE_GENERIC) e = hipMalloc(&d->scratch.p, (size_t)d->scratch_bytes_per_wave * mw);
         if (e != hipSuccess) {
             delete d;
             return fail(QPD_E_DEVICE, std::string("scratch hipMalloc: ") + hipGetErrorString(e));
@@ -277,6 +389,7 @@ int qpd_create(const qpd_config *c, qpd_decoder **out) {
             return fail(QPD_E_DEVICE, std::string("err hipMalloc: ") + hipGetErrorString(e));
         }
     }
+    if (d->engine == QPD_ENGINE_FAST) QPD_TRY(build_fast(d, c, s));
 #undef QPD_TRY
     P.lut_f = (const uint8_t *)d->lut_f.p;
     P.f_base = (const int32_t *)d->f_base.p;
@@ -305,6 +418,9 @@ int qpd_get_info(const qpd_decoder *d, qpd_info *info) {
     info->lanes_per_frame = d->plan.gs;
     info->max_waves = d->max_waves;
     info->scratch_bytes_per_wave = d->scratch_bytes_per_wave;
+    info->engine = d->engine;
+    info->lds_bytes_per_wave = d->lds_bytes;
+    info->lds_from_depth = d->engine == QPD_ENGINE_FAST ? d->fplan.lds_from : -1;
     return QPD_OK;
 }
 
@@ -319,6 +435,29 @@ int qpd_decode(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_o
     const int64_t groups = (B + d->plan.fpw - 1) / d->plan.fpw;
     const int grid = (int)std::min<int64_t>(groups, d->max_waves);
     hipStream_t st = (hipStream_t)stream;
+    if (d->engine == QPD_ENGINE_FAST) {
+        const int64_t fgroups = (B + d->fplan.fpw - 1) / d->fplan.fpw;
+        const int fgrid = (int)std::min<int64_t>(fgroups, d->max_waves);
+        const size_t lds = (size_t)d->lds_bytes;
+        switch (d->kind) {
+            case QPD_SC_LUT:
+                hipLaunchKernelGGL(qpd::lut_fast_kernel<qpd::K_SC_LUT>, dim3(fgrid), dim3(64), lds, st, d->fplan, d_symbols, B, d_out);
+                break;
+            case QPD_SCL_LUT:
+                hipLaunchKernelGGL(qpd::lut_fast_kernel<qpd::K_SCL_LUT>, dim3(fgrid), dim3(64), lds, st, d->fplan, d_symbols, B, d_out);
+                break;
+            case QPD_FASTSC_LUT:
+                hipLaunchKernelGGL(qpd::lut_fast_kernel<qpd::K_FASTSC_LUT>, dim3(fgrid), dim3(64), lds, st, d->fplan, d_symbols, B, d_out);
+                break;
+            case QPD_FASTSCL_LUT:
+                hipLaunchKernelGGL(qpd::lut_fast_kernel<qpd::K_FASTSCL_LUT>, dim3(fgrid), dim3(64), lds, st, d->fplan, d_symbols, B, d_out);
+                break;
+            default:
+                return fail(QPD_E_INVALID, "bad kind");
+        }
+        QPD_HIP(hipGetLastError());
+        return QPD_OK;
+    }
     switch (d->kind) {
         case QPD_SC_LUT:
             hipLaunchKernelGGL(qpd::lut_decode_kernel<qpd::K_SC_LUT>, dim3(grid), dim3(64), 0, st, d->plan, d_symbols, B, d_out);

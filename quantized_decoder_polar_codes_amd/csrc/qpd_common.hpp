@@ -1,0 +1,105 @@
+// qpd_common.hpp -- device-side pieces shared by the decode kernels:
+// schedule op encoding, list-pointer helpers, cross-lane helpers and the
+// survivor selection that reproduces the reference's mink tie order.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qpd {
+
+enum OpType : int32_t {
+    OP_F = 0,       // left child symbols  (f LUT), depth d -> d+1
+    OP_G = 1,       // right child symbols (g LUT), depth d -> d+1
+    OP_LEAF_L = 2,  // left leaf 2*node of a depth n-1 node (f LUT at j=0)
+    OP_LEAF_R = 3,  // right leaf 2*node+1                  (g LUT at j=0)
+    OP_COMB = 4,    // partial-sum combine u(), utils.cpp:62-67
+    OP_R0 = 5,
+    OP_R1 = 6,
+    OP_REP = 7,
+    OP_SPC = 8
+};
+
+struct Op {
+    int32_t type, d, node, aux;  // aux: frozen flag for leaves
+};
+
+constexpr int kMaxDepth = 16;  // N <= 65536
+constexpr int kMaxL = 8;       // 2L <= 16: libstdc++ sorts by insertion (stable)
+constexpr int kMaxM = kMaxL - 1;
+
+enum Kind : int32_t { K_SC_FLOAT = 0, K_SC_LUT = 1, K_SCL_LUT = 2, K_FASTSC_LUT = 3, K_FASTSCL_LUT = 4 };
+
+
+
+// ---------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t *row_ptr(uint32_t *wsc, int r) { return wsc + (size_t)r * 64; }
+
+__device__ __forceinline__ int ptr_get(uint64_t p, int d) { return (int)((p >> (4 * d)) & 15u); }
+
+__device__ __forceinline__ uint64_t ptr_set(uint64_t p, int d, int lane_in_group) {
+    const uint64_t m = 15ull << (4 * d);
+    return (p & ~m) | ((uint64_t)lane_in_group << (4 * d));
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t x, int src) {
+    uint32_t lo = __shfl((uint32_t)x, src);
+    uint32_t hi = __shfl((uint32_t)(x >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ double shfld(double x, int src) { return __shfl(x, src); }
+
+// Cross-lane reads (ds_bpermute) see 0 from lanes that are inactive for the
+// instruction, so every shuffle runs with the whole wave active: evaluate both
+// sides first, then select (never `c ? __shfl(a) : __shfl(b)`).
+__device__ __forceinline__ double pick(bool c, double a, double b) { return c ? a : b; }
+
+__device__ __forceinline__ void wave_sync() { __syncthreads(); }  // 64-thread block: one wave
+
+// Compiler-only ordering point for LDS accesses of a single wave.
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+
+
+
+
+// ---------------------------------------------------------------------------
+// Survivor selection: keep the L best of 2L candidates {keep_j = c_j,
+// flip_j = c_{j+L}} exactly as std::sort(index, key<) + take L (mink,
+// src/SCLLUTDecoder.cpp:8-21).  For 2L <= 16 libstdc++ runs a stable
+// insertion sort, i.e. order by (key, candidate index); rank each candidate by
+// counting the candidates before it, then invert the ranks through LDS.
+// ---------------------------------------------------------------------------
+struct Sel {
+    int parent;  // lane-in-group of the surviving candidate's path
+    bool upper;  // candidate came from the second half (flip / penalty branch)
+};
+
+__device__ __forceinline__ Sel select_survivors(double kk, double kf, int gl, int gbase, int L, int *sel) {
+    int rk = 0, rf = 0;
+    for (int j = 0; j < L; ++j) {
+        const double ok = shfld(kk, gbase + j);
+        const double of = shfld(kf, gbase + j);
+        rk += (ok < kk) || (ok == kk && j < gl);
+        rk += (of < kk);
+        rf += (ok <= kf);
+        rf += (of < kf) || (of == kf && j < gl);
+    }
+    if (gl < L) {
+        if (rk < L) sel[gbase + rk] = gl;
+        if (rf < L) sel[gbase + rf] = gl + L;
+    }
+    // One wave per workgroup and LDS instructions of a wave complete in order:
+    // the scatter above is visible to the gather below without s_barrier or a
+    // vmcnt drain (which would also stall on in-flight global prefetches).
+    lds_order();
+    int c = (gl < L) ? sel[gbase + gl] : gl;
+    lds_order();
+    Sel s;
+    s.upper = c >= L;
+    s.parent = s.upper ? c - L : c;
+    return s;
+}
+
+}  // namespace qpd

@@ -22,31 +22,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "qpd_common.hpp"
 #include "stl_sort.hpp"
 
 namespace qpd {
-
-enum OpType : int32_t {
-    OP_F = 0,       // left child symbols  (f LUT), depth d -> d+1
-    OP_G = 1,       // right child symbols (g LUT), depth d -> d+1
-    OP_LEAF_L = 2,  // left leaf 2*node of a depth n-1 node (f LUT at j=0)
-    OP_LEAF_R = 3,  // right leaf 2*node+1                  (g LUT at j=0)
-    OP_COMB = 4,    // partial-sum combine u(), utils.cpp:62-67
-    OP_R0 = 5,
-    OP_R1 = 6,
-    OP_REP = 7,
-    OP_SPC = 8
-};
-
-struct Op {
-    int32_t type, d, node, aux;  // aux: frozen flag for leaves
-};
-
-constexpr int kMaxDepth = 16;  // N <= 65536
-constexpr int kMaxL = 8;       // 2L <= 16: libstdc++ sorts by insertion (stable)
-constexpr int kMaxM = kMaxL - 1;
-
-enum Kind : int32_t { K_SC_FLOAT = 0, K_SC_LUT = 1, K_SCL_LUT = 2, K_FASTSC_LUT = 3, K_FASTSCL_LUT = 4 };
 
 struct DevPlan {
     int32_t N, n, K, L, v, gs, fpw, nops;
@@ -68,36 +47,10 @@ struct DevPlan {
     int32_t *err;
 };
 
-// ---------------------------------------------------------------------------
-// small helpers
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t *row_ptr(uint32_t *wsc, int r) { return wsc + (size_t)r * 64; }
-
-__device__ __forceinline__ int ptr_get(uint64_t p, int d) { return (int)((p >> (4 * d)) & 15u); }
-
-__device__ __forceinline__ uint64_t ptr_set(uint64_t p, int d, int lane_in_group) {
-    const uint64_t m = 15ull << (4 * d);
-    return (p & ~m) | ((uint64_t)lane_in_group << (4 * d));
-}
-
-__device__ __forceinline__ uint64_t shfl64(uint64_t x, int src) {
-    uint32_t lo = __shfl((uint32_t)x, src);
-    uint32_t hi = __shfl((uint32_t)(x >> 32), src);
-    return ((uint64_t)hi << 32) | lo;
-}
-
-__device__ __forceinline__ double shfld(double x, int src) { return __shfl(x, src); }
-
-// Cross-lane reads (ds_bpermute) see 0 from lanes that are inactive for the
-// instruction, so every shuffle runs with the whole wave active: evaluate both
-// sides first, then select (never `c ? __shfl(a) : __shfl(b)`).
-__device__ __forceinline__ double pick(bool c, double a, double b) { return c ? a : b; }
-
-__device__ __forceinline__ void wave_sync() { __syncthreads(); }  // 64-thread block: one wave
-
 __device__ __forceinline__ double vcl_at(const DevPlan &P, int row, int pos, int sym) {
     return P.vcl[((size_t)row * P.N + pos) * P.v + sym];
 }
+
 
 // Channel symbol read with range check (the reference has none: UB there).
 __device__ __forceinline__ int in_sym(const DevPlan &P, const int32_t *y, int e) {
@@ -109,6 +62,7 @@ __device__ __forceinline__ int in_sym(const DevPlan &P, const int32_t *y, int e)
     return s;
 }
 
+
 // Symbol e of the active node at depth d, for the path whose slot is `src`.
 __device__ __forceinline__ int node_sym(const DevPlan &P, uint32_t *wsc, const int32_t *y, int d, int src, int e) {
     if (d == 0) return in_sym(P, y, e);
@@ -116,40 +70,6 @@ __device__ __forceinline__ int node_sym(const DevPlan &P, uint32_t *wsc, const i
     return (int)((w >> (8 * (e & 3))) & 255u);
 }
 
-// ---------------------------------------------------------------------------
-// Survivor selection: keep the L best of 2L candidates {keep_j = c_j,
-// flip_j = c_{j+L}} exactly as std::sort(index, key<) + take L (mink,
-// src/SCLLUTDecoder.cpp:8-21).  For 2L <= 16 libstdc++ runs a stable
-// insertion sort, i.e. order by (key, candidate index); rank each candidate by
-// counting the candidates before it, then invert the ranks through LDS.
-// ---------------------------------------------------------------------------
-struct Sel {
-    int parent;  // lane-in-group of the surviving candidate's path
-    bool upper;  // candidate came from the second half (flip / penalty branch)
-};
-
-__device__ __forceinline__ Sel select_survivors(double kk, double kf, int gl, int gbase, int L, int *sel) {
-    int rk = 0, rf = 0;
-    for (int j = 0; j < L; ++j) {
-        const double ok = shfld(kk, gbase + j);
-        const double of = shfld(kf, gbase + j);
-        rk += (ok < kk) || (ok == kk && j < gl);
-        rk += (of < kk);
-        rf += (ok <= kf);
-        rf += (of < kf) || (of == kf && j < gl);
-    }
-    if (gl < L) {
-        if (rk < L) sel[gbase + rk] = gl;
-        if (rf < L) sel[gbase + rf] = gl + L;
-    }
-    wave_sync();
-    int c = (gl < L) ? sel[gbase + gl] : gl;
-    wave_sync();
-    Sel s;
-    s.upper = c >= L;
-    s.parent = s.upper ? c - L : c;
-    return s;
-}
 
 // Write the finished node's partial sums (nbits bits, in `words`) either to the
 // path's own U[d] slot (left child) or to the own R chain (right child / root).

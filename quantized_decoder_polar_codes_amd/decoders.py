@@ -46,7 +46,7 @@ class _DecoderBase:
     _float_input = False
 
     def __init__(self, N, K, L, frozen_bits, message_bits, node_type, packed: PackedLUT | None, device=None,
-                 max_waves: int = 0):
+                 max_waves: int = 0, engine: str = "auto"):
         self.N = int(N)
         self.K = int(K)
         self.L = int(L)
@@ -81,6 +81,8 @@ class _DecoderBase:
         self.device = int(device)
         cfg.device = self.device
         cfg.max_waves = int(max_waves)
+        cfg.engine = {"auto": _lib.QPD_ENGINE_AUTO, "generic": _lib.QPD_ENGINE_GENERIC,
+                      "fast": _lib.QPD_ENGINE_FAST}[engine]
         h = ctypes.c_void_p()
         _lib.check(lib.qpd_create(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h

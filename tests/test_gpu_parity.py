@@ -39,15 +39,23 @@ def _node_type(N, K):
     return fm, C.identify_nodes(N, mb).astype(np.int32)
 
 
+ENGINES = ["auto", "generic"]  # auto = the fast kernel wherever the tables allow it
+
+
+@pytest.mark.parametrize("engine", ENGINES)
 @pytest.mark.parametrize("path", golden_files(), ids=lambda p: os.path.basename(p)[:-4])
-def test_gpu_matches_golden(path, qpd):
+def test_gpu_matches_golden(path, engine, qpd):
     g = load_golden(path)
     N, K, L = int(g["N"]), int(g["K"]), int(g["L"])
     if str(g["kind"]) == "SC":
+        if engine != "auto":
+            pytest.skip("float SC has one kernel")
         dec = qpd.SCDecoder(N, K, g["frozen"], 1 - g["frozen"])
         got = dec.decode_batch(g["llr"])
     else:
-        dec = qpd.from_packed(str(g["kind"]), golden_packed(g), K, g["frozen"], L=L, node_type=g["node_type"])
+        dec = qpd.from_packed(str(g["kind"]), golden_packed(g), K, g["frozen"], L=L, node_type=g["node_type"],
+                              engine=engine)
+        assert dec.info()["engine"] == (2 if engine == "auto" else 1)
         got = dec.decode_batch(g["symbols"].astype(np.int32))
     bad = np.flatnonzero((got != g["expected"]).any(1))
     assert bad.size == 0, f"{bad.size}/{len(got)} frames differ, first {bad[:5]}"
@@ -70,9 +78,10 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("engine", ENGINES)
 @pytest.mark.parametrize("N,K,L,tables", CASES)
 @pytest.mark.parametrize("kind", KINDS)
-def test_gpu_matches_oracle(N, K, L, tables, kind, qpd, oracle_mod):
+def test_gpu_matches_oracle(N, K, L, tables, kind, engine, qpd, oracle_mod):
     from quantized_decoder_polar_codes_amd import lut as LU
 
     seed = 1000 + N + 7 * L + KINDS.index(kind)
@@ -90,10 +99,12 @@ def test_gpu_matches_oracle(N, K, L, tables, kind, qpd, oracle_mod):
         with pytest.raises(RuntimeError):
             oracle_mod.decode_lut(kind, p, K, L, fm, sym, node_type=nt)
         with pytest.raises(ValueError):
-            qpd.from_packed(kind, p, K, fm, L=L, node_type=nt)
+            qpd.from_packed(kind, p, K, fm, L=L, node_type=nt, engine=engine)
         return
     want = oracle_mod.decode_lut(kind, p, K, L, fm, sym, node_type=nt)
-    dec = qpd.from_packed(kind, p, K, fm, L=L, node_type=nt)
+    dec = qpd.from_packed(kind, p, K, fm, L=L, node_type=nt, engine=engine)
+    if engine == "auto":
+        assert dec.info()["engine"] == (1 if tables == "perelem" else 2)
     got = dec.decode_batch(sym)
     bad = np.flatnonzero((got != want).any(1))
     assert bad.size == 0, f"{bad.size}/{B} frames differ, first {bad[:5]}"
@@ -181,8 +192,9 @@ def _noiseless_symbols(msg, msgbits, N, v=16):
     return np.where(x == 0, v - 1, 0).astype(np.int32)  # strongest +/- quanta
 
 
+@pytest.mark.parametrize("engine", ENGINES)
 @pytest.mark.parametrize("kind", KINDS)
-def test_full_size_noiseless_roundtrip(kind, qpd):
+def test_full_size_noiseless_roundtrip(kind, engine, qpd):
     """BASELINE size (N=1024, K=512, L=8): encode -> noiseless channel -> decode
     returns every message, over 2^16 frames (SCL) / 2^17 (SC)."""
     from quantized_decoder_polar_codes_amd import codes as C
@@ -194,12 +206,13 @@ def test_full_size_noiseless_roundtrip(kind, qpd):
     B = 1 << (16 if "SCL" in kind else 17)
     msg = np.random.default_rng(11).integers(0, 2, size=(B, K), dtype=np.uint8)
     sym = _noiseless_symbols(msg, mb, N)
-    d = qpd.from_packed(kind, LU.minsum_uniform_luts(N), K, fm, L=L, node_type=nt)
+    d = qpd.from_packed(kind, LU.minsum_uniform_luts(N), K, fm, L=L, node_type=nt, engine=engine)
     got = d.decode_batch(sym)
     assert (got == msg).all()
 
 
-def test_batch_and_grid_invariance(qpd):
+@pytest.mark.parametrize("engine", ENGINES)
+def test_batch_and_grid_invariance(engine, qpd):
     """A frame's bits do not depend on its batch neighbours, the batch size or
     the persistent-grid size (grid-stride path)."""
     from quantized_decoder_polar_codes_amd import lut as LU
@@ -208,8 +221,38 @@ def test_batch_and_grid_invariance(qpd):
     p = LU.random_luts(N, 16, seed=21, distinct_mags=3)
     fm, nt = _node_type(N, K)
     sym = np.random.default_rng(3).integers(0, 16, size=(517, N), dtype=np.int32)
-    a = qpd.from_packed("FastSCL-LUT", p, K, fm, L=L, node_type=nt).decode_batch(sym)
-    b = qpd.from_packed("FastSCL-LUT", p, K, fm, L=L, node_type=nt, max_waves=3).decode_batch(sym)
-    c = qpd.from_packed("FastSCL-LUT", p, K, fm, L=L, node_type=nt).decode_batch(sym[100:107])
+    mk = lambda **kw: qpd.from_packed("FastSCL-LUT", p, K, fm, L=L, node_type=nt, engine=engine, **kw)  # noqa: E731
+    a = mk().decode_batch(sym)
+    b = mk(max_waves=3).decode_batch(sym)
+    c = mk().decode_batch(sym[100:107])
     assert (a == b).all()
     assert (a[100:107] == c).all()
+
+
+def test_fast_engine_lds_placement_sweep(qpd, oracle_mod, monkeypatch):
+    """Every split of the tree between LDS and global scratch gives the same bits."""
+    from quantized_decoder_polar_codes_amd import lut as LU
+
+    N, K, L = 256, 128, 4
+    p = LU.random_luts(N, 16, seed=55, distinct_mags=3)
+    fm, nt = _node_type(N, K)
+    sym = np.random.default_rng(56).integers(0, 16, size=(80, N), dtype=np.int32)
+    for kind in ("SCL-LUT", "FastSCL-LUT", "FastSC-LUT"):
+        want = oracle_mod.decode_lut(kind, p, K, L, fm, sym, node_type=nt)
+        seen = set()
+        for budget in (256, 1024, 2048, 4096, 8192, 65536):
+            monkeypatch.setenv("QPD_LDS_BUDGET", str(budget))
+            d = qpd.from_packed(kind, p, K, fm, L=L, node_type=nt, engine="fast")
+            seen.add(d.info()["lds_from_depth"])
+            assert (d.decode_batch(sym) == want).all(), (kind, budget)
+        assert len(seen) >= 4
+
+
+def test_fast_engine_rejects_per_element_tables(qpd):
+    from quantized_decoder_polar_codes_amd import lut as LU
+
+    N, K = 32, 16
+    p = LU.random_luts(N, 16, seed=3, per_element=True)
+    fm, nt = _node_type(N, K)
+    with pytest.raises(ValueError):
+        qpd.from_packed("SCL-LUT", p, K, fm, L=4, engine="fast")
