@@ -113,6 +113,7 @@ def test_pack_validation_errors():
 
 def _header_functions():
     txt = open(os.path.join(ROOT, "include", "qpd.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)  # drop comments
     return sorted(set(re.findall(r"\b(qpd_[a-z0-9_]+)\s*\(", txt)))
 
 
