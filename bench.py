@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--max-waves", type=int, default=0)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--parity-frames", type=int, default=8)
+    ap.add_argument("--engine", default="auto", choices=["auto", "fast", "generic"])
     return ap.parse_args()
 
 
@@ -121,7 +121,9 @@ def main():
     _, mb, fm, mm = C.construct_pw(N, K)
     nt = C.identify_nodes(N, mb).astype(np.int32)
     packed = LU.minsum_uniform_luts(N, v=16, delta=0.5)
-    dec = Q.from_packed(args.kind, packed, K, fm, L=L, node_type=nt, device=dev.index, max_waves=args.max_waves)
+    dec = Q.from_packed(args.kind, packed, K, fm, L=L, node_type=nt, device=dev.index, max_waves=args.max_waves,
+                        engine=args.engine)
+    info = dec.info()
     # rank r owns global frames [r*F, (r+1)*F): seed by rank -> disjoint frame sets
     msg, sym = synth_frames(N, K, args.frames, args.ebn0, 1234 + rank, mb)
     d_sym = torch.from_numpy(sym).to(dev)
@@ -191,7 +193,10 @@ def main():
                     "synthetic saturating min-sum 16-level LUTs; resident in HBM",
             "config": {"workload": f"{args.kind} N={N} K={K} L={L} Q=16 (5G-NR PW code, no CRC)",
                        "decoder": args.kind, "N": N, "K": K, "L": L, "v": 16, "frames_per_gpu_per_step": args.frames,
-                       "ebn0_db": args.ebn0, "parallelism": f"dp{world} (frames sharded, RCCL counter all-reduce)"},
+                       "ebn0_db": args.ebn0, "parallelism": f"dp{world} (frames sharded, RCCL counter all-reduce)",
+                       "engine": {1: "generic", 2: "fast"}[info["engine"]], "lds_bytes_per_wave": info["lds_bytes_per_wave"],
+                       "lds_from_depth": info["lds_from_depth"], "waves": min(info["max_waves"],
+                       -(-args.frames // info["frames_per_wave"]))},
             "ber": bit_errs / max(1, frames_all * K),
             "bler": blk_errs / max(1, frames_all),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

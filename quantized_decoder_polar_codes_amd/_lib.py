@@ -10,7 +10,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libqpd.so")
+LIB_PATH = os.environ.get("QPD_LIB") or os.path.join(HERE, "libqpd.so")
 
 QPD_SC_FLOAT, QPD_SC_LUT, QPD_SCL_LUT, QPD_FASTSC_LUT, QPD_FASTSCL_LUT = range(5)
 QPD_ENGINE_AUTO, QPD_ENGINE_GENERIC, QPD_ENGINE_FAST = range(3)

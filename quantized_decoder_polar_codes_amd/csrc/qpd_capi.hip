@@ -104,7 +104,8 @@ struct qpd_decoder {
     int lds_bytes = 0;
     DevPlan plan{};
     qpd::FastPlan fplan{};
-    DeviceBuf f_tab, g_tab, fscratch;
+    DeviceBuf f_tab, g_tab, fscratch, mops;
+    int num_mops = 0;
     std::vector<Op> ops_host;
     DeviceBuf lut_f, f_base, lut_g, g_base, vcl, ops, info_pos, scratch, err;
     // staging for the host-buffer entry points
@@ -174,9 +175,117 @@ int validate(const qpd_config *c, int *n_out) {
 }
 
 
-// Fast-engine plan (qpd_fast.hip): nibble-packed per-node tables and the
-// per-depth placement of the path buffers (deep levels in LDS, shallow levels
-// in a global scratch slab), sized to the LDS budget per wave.
+// Fast-engine plan (qpd_fast.hip): per-depth placement of the path buffers
+// (deep levels in LDS, shallow levels in a global slab, sized to the LDS
+// budget per wave), nibble-packed per-node tables, and the micro-op list with
+// every offset precomputed and plain height-3 subtrees fused into BOT3 ops.
+struct FastLayout {
+    int D = 0;
+    int S[qpd::kMaxDepth + 1] = {}, U[qpd::kMaxDepth + 1] = {}, R[qpd::kMaxDepth + 1] = {};
+    bool lds(int dd) const { return dd >= D; }
+};
+
+void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N, int n, int v, const int32_t *frozen,
+              const int32_t *node_type, int d, int node) {
+    using namespace qpd;
+    const int posi = (1 << d) + node - 1;
+    auto base = [&](int type) {
+        MOp m;
+        std::memset(&m, 0, sizeof(m));
+        m.type = type;
+        m.d = d;
+        m.node = node;
+        m.sh_src = 4 * d;
+        if (d == 0)
+            m.flags |= MF_CHAN;
+        else {
+            m.src_row = Ly.S[d];
+            if (Ly.lds(d)) m.flags |= MF_SRC_LDS;
+        }
+        return m;
+    };
+    auto finish_node = [&](MOp &m) {  // destination of a finished node (d, node)
+        const bool to_r = d == 0 || (node & 1);
+        m.dst_row = to_r ? Ly.R[d] : Ly.U[d];
+        if (to_r) m.flags |= MF_TO_R;
+        if (Ly.lds(d)) m.flags |= MF_DST_LDS;
+        else m.flags |= MF_SYNC;
+        m.sh_dst = 4 * d;
+    };
+    const int t = special_of(kind, node_type, posi);
+    if (t >= 0) {
+        MOp m = base(OP_R0 + t);
+        m.cnt = N >> d;
+        m.vrow = (d - 1) * N + (N >> d) * node;
+        finish_node(m);
+        out.push_back(m);
+        return;
+    }
+    if (n >= 3 && d == n - 3) {
+        bool plain = true;
+        for (int dd = d; dd < n; ++dd)
+            for (int k = 0; k < (1 << (dd - d)); ++k)
+                plain = plain && special_of(kind, node_type, (1 << dd) + (node << (dd - d)) + k - 1) < 0;
+        if (plain) {
+            MOp m = base(OP_BOT3);
+            for (int j = 0; j < 8; ++j) m.cnt |= (frozen[8 * node + j] == 1) << j;
+            m.tab = posi;
+            m.vrow = ((n - 1) * N + 8 * node) * v;
+            finish_node(m);
+            out.push_back(m);
+            return;
+        }
+    }
+    if (d + 1 < n) {
+        for (int side = 0; side < 2; ++side) {
+            MOp m = base(side ? OP_G : OP_F);
+            m.cnt = N >> (d + 1);
+            m.dst_row = Ly.S[d + 1];
+            if (Ly.lds(d + 1)) m.flags |= MF_DST_LDS;
+            else m.flags |= MF_SYNC;
+            m.sh_dst = 4 * (d + 1);
+            if (side) {
+                m.u_row = Ly.U[d + 1];
+                if (Ly.lds(d + 1)) m.flags |= MF_U_LDS;
+                m.sh_u = 4 * (d + 1);
+                m.tab = posi * 64;
+            } else {
+                m.tab = posi * 32;
+            }
+            out.push_back(m);
+            fast_ops(out, Ly, kind, N, n, v, frozen, node_type, d + 1, 2 * node + side);
+        }
+    } else {
+        for (int side = 0; side < 2; ++side) {
+            const int k = 2 * node + side;
+            MOp m = base(side ? OP_LEAF_R : OP_LEAF_L);
+            m.cnt = frozen[k] == 1;
+            m.dst_row = side ? Ly.R[n] : Ly.U[n];
+            if (Ly.lds(n)) m.flags |= MF_DST_LDS;
+            else m.flags |= MF_SYNC;
+            m.sh_dst = 4 * n;
+            if (side) {
+                m.u_row = Ly.U[n];
+                if (Ly.lds(n)) m.flags |= MF_U_LDS;
+                m.sh_u = 4 * n;
+                m.tab = posi * 64;
+            } else {
+                m.tab = posi * 32;
+            }
+            m.vrow = ((n - 1) * N + k) * v;
+            out.push_back(m);
+        }
+    }
+    MOp m = base(OP_COMB);
+    m.cnt = N >> (d + 1);
+    m.u_row = Ly.U[d + 1];
+    m.r_row = Ly.R[d + 1];
+    if (Ly.lds(d + 1)) m.flags |= MF_U_LDS | MF_R_LDS;
+    m.sh_u = 4 * (d + 1);
+    finish_node(m);
+    out.push_back(m);
+}
+
 int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     qpd::FastPlan &F = d->fplan;
     const int N = c->N, n = d->n, v = c->v;
@@ -187,7 +296,6 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     F.v = v;
     F.gs = d->plan.gs;
     F.fpw = d->plan.fpw;
-    F.nops = (int)s.ops.size();
     F.max_r1 = s.max_r1;
     auto srows = [&](int dd) { return std::max(1, (N >> dd) / 8); };
     auto brows = [&](int dd) { return std::max(1, (N >> dd) / 32); };
@@ -198,28 +306,29 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
         for (int dd = D; dd <= n; ++dd) r += brows(dd);
         return r;
     };
-    int budget = 16 * 1024;
+    int budget = 6 * 1024;  // measured best on MI355X: occupancy beats LDS residency of depths < 5
     if (const char *e = getenv("QPD_LDS_BUDGET")) budget = atoi(e);
-    int D = 0;
-    while (D <= n && 256 + lds_rows(D) * 256 > budget) ++D;
-    F.lds_from = D;
+    FastLayout Ly;
+    while (Ly.D <= n && 256 + lds_rows(Ly.D) * 256 > budget) ++Ly.D;
+    F.lds_from = Ly.D;
     int rl = 0, rg = 0;
-    for (int dd = 0; dd <= qpd::kMaxDepth; ++dd) F.S_row[dd] = F.U_row[dd] = F.R_row[dd] = 0;
     for (int dd = 1; dd <= n - 1; ++dd) {
-        int &r = dd >= D ? rl : rg;
-        F.S_row[dd] = r;
+        int &r = Ly.lds(dd) ? rl : rg;
+        Ly.S[dd] = r;
         r += srows(dd);
     }
     for (int dd = 1; dd <= n; ++dd) {
-        int &r = dd >= D ? rl : rg;
-        F.U_row[dd] = r;
+        int &r = Ly.lds(dd) ? rl : rg;
+        Ly.U[dd] = r;
         r += brows(dd);
     }
     for (int dd = 0; dd <= n; ++dd) {
-        int &r = dd >= D ? rl : rg;
-        F.R_row[dd] = r;
+        int &r = Ly.lds(dd) ? rl : rg;
+        Ly.R[dd] = r;
         r += brows(dd);
     }
+    F.R0_row = Ly.R[0];
+    F.R0_lds = Ly.lds(0);
     F.H_row = F.K_row = F.I_row = rg;
     if (c->kind == QPD_FASTSCL_LUT && s.max_r1 > 0) {
         F.H_row = rg;
@@ -232,6 +341,15 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     F.lds_rows = rl;
     F.glb_rows = std::max(rg, 1);
     d->lds_bytes = 256 + rl * 256;
+    std::vector<qpd::MOp> mops;
+    fast_ops(mops, Ly, c->kind, N, n, v, c->frozen_bits,
+             (c->kind == QPD_FASTSC_LUT || c->kind == QPD_FASTSCL_LUT) ? c->node_type : nullptr, 0, 0);
+    F.nops = (int)mops.size();
+    d->num_mops = F.nops;
+    {
+        int rc = upload(d->mops, mops.data(), mops.size());
+        if (rc) return rc;
+    }
     // nibble-packed tables: entry (u, a, b) of node p at bit 4*(idx&7) of dword idx>>3
     std::vector<uint32_t> ft((size_t)(N - 1) * 32, 0), gt((size_t)(N - 1) * 64, 0);
     const size_t vv = (size_t)v * v;
@@ -253,7 +371,22 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     rc = upload(d->g_tab, gt.data(), gt.size());
     if (rc) return rc;
     const int64_t per_wave = (int64_t)F.glb_rows * 64 * 4;
-    int mw = c->max_waves > 0 ? c->max_waves : 256 * 12;
+    // Persistent grid: as many waves as can be resident at once.
+    int mw = c->max_waves;
+    if (mw <= 0) {
+        int dev = 0, ncu = 256, per_cu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        hipError_t oe = hipErrorInvalidValue;
+        switch (c->kind) {
+            case QPD_SC_LUT: oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, qpd::lut_fast_kernel<qpd::K_SC_LUT>, 64, d->lds_bytes); break;
+            case QPD_SCL_LUT: oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, qpd::lut_fast_kernel<qpd::K_SCL_LUT>, 64, d->lds_bytes); break;
+            case QPD_FASTSC_LUT: oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, qpd::lut_fast_kernel<qpd::K_FASTSC_LUT>, 64, d->lds_bytes); break;
+            default: oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, qpd::lut_fast_kernel<qpd::K_FASTSCL_LUT>, 64, d->lds_bytes); break;
+        }
+        if (oe != hipSuccess || per_cu <= 0) per_cu = 16;
+        mw = std::max(1, ncu) * per_cu;
+    }
     mw = (int)std::max<int64_t>(1, std::min<int64_t>(mw, ((int64_t)2 << 30) / per_wave));
     d->max_waves = mw;
     d->scratch_bytes_per_wave = per_wave;
@@ -261,11 +394,10 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     F.f_tab = (const uint32_t *)d->f_tab.p;
     F.g_tab = (const uint32_t *)d->g_tab.p;
     F.vcl = (const double *)d->vcl.p;
-    F.ops = (const Op *)d->ops.p;
+    F.ops = (const qpd::MOp *)d->mops.p;
     F.info_pos = (const int32_t *)d->info_pos.p;
     F.scratch = (uint32_t *)d->fscratch.p;
     F.err = (int32_t *)d->err.p;
-    F.nops = (int)s.ops.size();
     return QPD_OK;
 }
 
@@ -413,7 +545,7 @@ int qpd_get_info(const qpd_decoder *d, qpd_info *info) {
     info->K = d->K;
     info->L = d->L;
     info->v = d->v;
-    info->num_ops = (int32_t)d->ops_host.size();
+    info->num_ops = d->engine == QPD_ENGINE_FAST ? d->num_mops : (int32_t)d->ops_host.size();
     info->frames_per_wave = d->plan.fpw;
     info->lanes_per_frame = d->plan.gs;
     info->max_waves = d->max_waves;
@@ -437,7 +569,10 @@ int qpd_decode(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_o
     hipStream_t st = (hipStream_t)stream;
     if (d->engine == QPD_ENGINE_FAST) {
         const int64_t fgroups = (B + d->fplan.fpw - 1) / d->fplan.fpw;
-        const int fgrid = (int)std::min<int64_t>(fgroups, d->max_waves);
+        int fgrid = (int)std::min<int64_t>(fgroups, d->max_waves);
+        // even out the rounds of the grid-stride loop (no partial last round)
+        const int64_t rounds = (fgroups + fgrid - 1) / fgrid;
+        fgrid = (int)((fgroups + rounds - 1) / rounds);
         const size_t lds = (size_t)d->lds_bytes;
         switch (d->kind) {
             case QPD_SC_LUT:

@@ -1,26 +1,26 @@
-// qpd_fast.hip -- the fast gfx950 LUT decode kernel (dedicated tables, v <= 16).
+// qpd_fast.hip -- the fast gfx950 LUT decode kernel (one table per node, v <= 16).
 //
-// Same algorithm, schedule and list management as the generic kernel
+// Same algorithm, traversal and list management as the generic kernel
 // (qpd_generic.hip: one lane per list path, G = pow2 >= L lanes per frame,
 // per-depth 4-bit slot pointers instead of deep copies), laid out for the
-// CDNA4 memory hierarchy:
+// CDNA4 memory hierarchy and for instruction count:
 //
-//  * Symbols are 4-bit nibbles, 8 per dword.  Per tree depth d the path's
-//    buffers are S[d] (symbols of the active depth-d node, N>>d nibbles),
-//    U[d] (partial sums of the finished left child, N>>d bits) and R[d]
-//    (partial sums of a finished right child, consumed by the next combine).
-//  * Deep levels (d >= lds_from) -- where almost all ops and all the latency-
-//    bound small ops live -- sit in LDS, laid out [row][64 lanes] so a wave's
-//    row access hits 64 distinct banks; a cross-lane (pointer) read stays in
-//    the same row.  Within one wave LDS instructions complete in order, so no
-//    barrier is needed between an op and the next one that reads its results.
-//  * Shallow levels (a few large ops per frame) sit in a per-wave global
-//    scratch slab with the same row layout; ops that write it end with a
-//    vmcnt drain before the next cross-lane read.
-//  * The f/g tables of the current node are held in ONE VGPR per lane (f:
-//    256 nibbles = 32 dwords, g: 512 nibbles = 64 dwords) and read with
-//    ds_bpermute (no LDS storage, no bank conflicts); the next op's table and
-//    leaf quanta row are prefetched while the current op runs.
+//  * Host-compiled micro-op records (MOp, 64 B, one s_load_dwordx16 each)
+//    carry every row offset, shift and flag an op needs, so the wave-uniform
+//    interpreter does almost no scalar arithmetic per op.
+//  * Symbols are 4-bit nibbles, 8 per dword.  Per tree depth d a path owns
+//    S[d] (symbols of the active depth-d node), U[d] (partial sums of the
+//    finished left child) and R[d] (partial sums of a finished right child).
+//    Deep levels (d >= lds_from) sit in LDS, shallow levels in a per-wave
+//    global slab; both are laid out [row][64 lanes].  LDS instructions of one
+//    wave complete in order, so LDS-only ops need no barrier.
+//  * The last three tree levels of every plain subtree are one BOT3 op held
+//    entirely in registers: 8 symbols in, 8 leaves decided (with list forks
+//    moving the whole in-register state from the parent lane), 8 partial-sum
+//    bits out -- 21 interpreted ops become one straight-line block.
+//  * The current node's f/g table sits in ONE VGPR per lane (f: 256 nibbles =
+//    32 dwords, g: 512 nibbles = 64 dwords), read with ds_bpermute; the next
+//    op's table / leaf quanta row are prefetched while the current op runs.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -30,16 +30,42 @@
 
 namespace qpd {
 
+constexpr int OP_BOT3 = 9;  // fused bottom subtree of height 3 (fast engine only)
+
+enum MopFlag : int32_t {
+    MF_SRC_LDS = 1,   // S[d] in LDS
+    MF_DST_LDS = 2,   // destination rows in LDS
+    MF_U_LDS = 4,     // U rows read by the op in LDS
+    MF_TO_R = 8,      // finished node is a right child (or the root): write R, not U
+    MF_SYNC = 16,     // op touched the global slab: drain before the next op
+    MF_R_LDS = 32,    // R rows read by the op (COMB) in LDS
+    MF_CHAN = 64,     // S[d] is the channel input (d == 0)
+};
+
+struct MOp {
+    int32_t type, flags, d, node;
+    int32_t cnt;      // F/G/COMB: ctemp = N>>(d+1); special: temp = N>>d; LEAF: frozen; BOT3: frozen mask
+    int32_t src_row;  // S[d]
+    int32_t dst_row;  // F/G: S[d+1]; COMB/special/BOT3: U[d] or R[d]; LEAF_L: U[n]; LEAF_R: R[n]
+    int32_t u_row;    // G/COMB: U[d+1]; LEAF_R: U[n]
+    int32_t r_row;    // COMB: R[d+1]
+    int32_t sh_src;   // 4*d: ps field of S[d]
+    int32_t sh_u;     // G/COMB: 4*(d+1); LEAF_R: 4*n
+    int32_t sh_dst;   // F/G: 4*(d+1) (ps); COMB/special/BOT3 left child: 4*d (pu); LEAF_L: 4*n (pu)
+    int32_t tab;      // F/LEAF_L: posi*32; G/LEAF_R: posi*64; BOT3: posi of the subtree root
+    int32_t vrow;     // LEAF: ((n-1)*N + k)*v; special: (d-1)*N + temp*node; BOT3: ((n-1)*N + 8*node)*v
+    int32_t pad0, pad1;
+};
+
 struct FastPlan {
     int32_t N, n, K, L, v, gs, fpw, nops, max_r1;
     int32_t lds_rows, glb_rows, lds_from;
-    // per-depth buffer rows; depth d lives in LDS iff d >= lds_from
-    int32_t S_row[kMaxDepth + 1], U_row[kMaxDepth + 1], R_row[kMaxDepth + 1];
+    int32_t R0_row, R0_lds;      // root partial sums (R[0])
     int32_t H_row, K_row, I_row;  // R1 scratch (global)
     const uint32_t *f_tab;        // [N-1][32] nibble-packed f tables
     const uint32_t *g_tab;        // [N-1][64] nibble-packed g tables (u=0: dwords 0..31)
     const double *vcl;            // [rows][N][v]
-    const Op *ops;
+    const MOp *ops;
     const int32_t *info_pos;
     uint32_t *scratch;            // [waves][glb_rows][64]
     int32_t *err;
@@ -69,6 +95,11 @@ __device__ __forceinline__ uint32_t lut4(uint32_t table, uint32_t idx) {
     return (bperm(table, idx >> 3) >> ((idx & 7u) << 2)) & 15u;
 }
 
+__device__ __forceinline__ int pfield(uint64_t p, int sh) { return (int)((p >> sh) & 15u); }
+__device__ __forceinline__ uint64_t pset(uint64_t p, int sh, int gl) {
+    return (p & ~(15ull << sh)) | ((uint64_t)gl << sh);
+}
+
 // Channel symbols: int32 input, range-checked (UB in the reference).
 __device__ __forceinline__ uint32_t chan_sym(const int32_t *y, int e, int v, int32_t *err) {
     int s = y[e];
@@ -79,54 +110,32 @@ __device__ __forceinline__ uint32_t chan_sym(const int32_t *y, int e, int v, int
     return (uint32_t)s;
 }
 
-// 8 consecutive channel symbols packed as nibbles.
 __device__ __forceinline__ uint32_t chan_word(const int32_t *y, int e0, int cnt, int v, int32_t *err) {
     uint32_t w = 0;
     for (int i = 0; i < cnt; ++i) w |= chan_sym(y, e0 + i, v, err) << (4 * i);
     return w;
 }
 
-// Symbol e of the active node at depth d of the path whose slot is `src`.
-__device__ __forceinline__ uint32_t node_sym4(const FastPlan &P, const Mem &M, const int32_t *y, int d, int src,
-                                              int e) {
-    if (d == 0) return chan_sym(y, e, P.v, P.err);
-    const uint32_t w = M.ld(d >= P.lds_from, P.S_row[d] + (e >> 3), src);
-    return (w >> ((e & 7) << 2)) & 15u;
+// Word w (8 symbols) of S[d] of the path whose slot is `src`.
+__device__ __forceinline__ uint32_t sym_word(const FastPlan &P, const Mem &M, const MOp &op, const int32_t *y, int src,
+                                             int w, int cnt = 8) {
+    if (op.flags & MF_CHAN) return chan_word(y, 8 * w, cnt, P.v, P.err);
+    return M.ld(op.flags & MF_SRC_LDS, op.src_row + w, src);
 }
 
-__device__ __forceinline__ double vcl_at4(const FastPlan &P, int row, int pos, int sym) {
-    return P.vcl[((size_t)row * P.N + pos) * P.v + sym];
-}
-
-// Write word w of a finished node's partial sums: left child -> own U[d],
-// right child (or root) -> own R[d].
-__device__ __forceinline__ void put_node(const FastPlan &P, const Mem &M, int d, bool to_r, int w, uint32_t word,
-                                         int lane) {
-    const bool l = d >= P.lds_from;
-    M.st(l, (to_r ? P.R_row[d] : P.U_row[d]) + w, lane, word);
-}
-
-// f / g op: compute the left (f) or right (g) child symbols at depth d+1 of
-// the active node at depth d (SCLLUTDecoder.cpp:83-89 / :157-164).
+// f / g op (SCLLUTDecoder.cpp:83-89 / :157-164): child symbols at depth d+1.
 template <bool ISG>
-__device__ __forceinline__ void fg_op(const FastPlan &P, const Mem &M, const int32_t *y, int d, int src, int usrc,
-                                      uint32_t T, int lane) {
-    const int ctemp = P.N >> (d + 1);
-    const bool sl = d >= P.lds_from, dl = (d + 1) >= P.lds_from, ul = (d + 1) >= P.lds_from;
-    const int so = P.S_row[d], to = P.S_row[d + 1], uo = P.U_row[d + 1];
+__device__ __forceinline__ void fg_op(const FastPlan &P, const Mem &M, const MOp &op, const int32_t *y, int src,
+                                      int usrc, uint32_t T, int lane) {
+    const int ctemp = op.cnt;
+    const bool dl = op.flags & MF_DST_LDS, ul = op.flags & MF_U_LDS;
     if (ctemp >= 8) {
         const int nwo = ctemp >> 3;
         for (int w = 0; w < nwo; ++w) {
-            uint32_t A, B;
-            if (d == 0) {
-                A = chan_word(y, 8 * w, 8, P.v, P.err);
-                B = chan_word(y, ctemp + 8 * w, 8, P.v, P.err);
-            } else {
-                A = M.ld(sl, so + w, src);
-                B = M.ld(sl, so + nwo + w, src);
-            }
+            const uint32_t A = sym_word(P, M, op, y, src, w);
+            const uint32_t B = sym_word(P, M, op, y, src, nwo + w);
             uint32_t ub = 0;
-            if (ISG) ub = (M.ld(ul, uo + (w >> 2), usrc) >> ((w & 3) << 3)) << 8;
+            if (ISG) ub = (M.ld(ul, op.u_row + (w >> 2), usrc) >> ((w & 3) << 3)) << 8;
             uint32_t out = 0;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -134,18 +143,18 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem &M, const int
                 if (ISG) idx |= (ub >> i) & 256u;
                 out |= lut4(T, idx) << (4 * i);
             }
-            M.st(dl, to + w, lane, out);
+            M.st(dl, op.dst_row + w, lane, out);
         }
     } else {  // ctemp in {2, 4}: the whole depth-d node (a then b) is one word
-        const uint32_t W = (d == 0) ? chan_word(y, 0, 2 * ctemp, P.v, P.err) : M.ld(sl, so, src);
-        uint32_t ub = ISG ? M.ld(ul, uo, usrc) : 0u;
+        const uint32_t W = sym_word(P, M, op, y, src, 0, 2 * ctemp);
+        const uint32_t ub = ISG ? M.ld(ul, op.u_row, usrc) : 0u;
         uint32_t out = 0;
         for (int i = 0; i < ctemp; ++i) {
             uint32_t idx = (((W >> (4 * i)) & 15u) << 4) | ((W >> (4 * (i + ctemp))) & 15u);
             if (ISG) idx |= ((ub >> i) & 1u) << 8;
             out |= lut4(T, idx) << (4 * i);
         }
-        M.st(dl, to, lane, out);
+        M.st(dl, op.dst_row, lane, out);
     }
 }
 
@@ -165,27 +174,159 @@ struct Pre {
     double V;    // leaf: vcl row entry of this lane (lanes < v)
 };
 
-__device__ __forceinline__ Pre fetch_pre(const FastPlan &P, const Op &op, int lane) {
+__device__ __forceinline__ Pre fetch_pre(const FastPlan &P, const MOp &op, int lane, int vlane) {
     Pre p;
     p.T = 0;
     p.V = 0;
-    const int posi = (1 << op.d) + op.node - 1;
-    if (op.type == OP_F || op.type == OP_LEAF_L) {
-        p.T = P.f_tab[(size_t)posi * 32 + (lane & 31)];
-    } else if (op.type == OP_G || op.type == OP_LEAF_R) {
-        p.T = P.g_tab[(size_t)posi * 64 + lane];
-    }
-    if (op.type == OP_LEAF_L || op.type == OP_LEAF_R) {
-        const int k = 2 * op.node + (op.type == OP_LEAF_R);
-        const int s = lane < P.v ? lane : 0;
-        p.V = P.vcl[((size_t)(P.n - 1) * P.N + k) * P.v + s];
-    }
+    if (op.type == OP_F || op.type == OP_LEAF_L) p.T = P.f_tab[op.tab + (lane & 31)];
+    if (op.type == OP_G || op.type == OP_LEAF_R) p.T = P.g_tab[op.tab + lane];
+    if (op.type == OP_BOT3) p.T = P.f_tab[op.tab * 32 + (lane & 31)];
+    if (op.type == OP_LEAF_L || op.type == OP_LEAF_R) p.V = P.vcl[op.vrow + vlane];
     return p;
 }
 
+// ---------------------------------------------------------------------------
+// List state and the fork (mink, SCLLUTDecoder.cpp:105-144)
+// ---------------------------------------------------------------------------
+struct Path {
+    double pm;
+    uint64_t ps, pu;
+};
+
+// Info leaf with quanta dm: keep the L best of {keep, flip} candidates.
+// Returns the new decision; `extra` words follow the surviving lineage.
+template <int NX>
+__device__ __forceinline__ uint32_t leaf_fork(Path &st, double dm, int gl, int gbase, int L, int *sel,
+                                              uint32_t (&extra)[NX]) {
+    const double kf = st.pm + fabs(dm);
+    const Sel sl = select_survivors(st.pm, kf, gl, gbase, L, sel);
+    const int p = gbase + sl.parent;
+    const uint32_t hd = dm < 0;  // H4: SCL family `< 0`
+    const uint32_t dec = (uint32_t)__shfl((int)hd, p) ^ (sl.upper ? 1u : 0u);
+    st.pm = pick(sl.upper, shfld(kf, p), shfld(st.pm, p));
+    st.ps = shfl64(st.ps, p);
+    st.pu = shfl64(st.pu, p);
+#pragma unroll
+    for (int i = 0; i < NX; ++i) extra[i] = (uint32_t)__shfl((int)extra[i], p);
+    return dec;
+}
+
+// One leaf decision.  `frozen` is wave-uniform.
+template <bool kList, int NX>
+__device__ __forceinline__ uint32_t leaf_decide(Path &st, double dm, bool frozen, int gl, int gbase, int L, int *sel,
+                                                uint32_t (&extra)[NX]) {
+    if (!kList) return frozen ? 0u : (uint32_t)(dm <= 0);  // H4: SC family `<= 0`
+    if (frozen) {
+        st.pm += fabs(dm) * (double)(dm < 0);  // :100-104
+        return 0u;
+    }
+    return leaf_fork(st, dm, gl, gbase, L, sel, extra);
+}
+
+// ---------------------------------------------------------------------------
+// BOT3: the height-3 subtree under a depth n-3 node, fully in registers.
+// Node numbering inside the subtree (posi): q0 = p0; q1,q2 = 2p0+1, 2p0+2;
+// q3..q6 = 4p0+3 .. 4p0+6; leaves k0..k0+7 (k0 = 8*node).
+// In-register lineage state: W3 (8 symbols of q0) and pk = W2 (bits 0-15, 4
+// symbols of the current depth n-2 node) | W1 (bits 16-23, 2 symbols) |
+// bL (bit 24, left leaf decision) | c2 (bits 25-26, left result at depth n-1)
+// | c3 (bits 27-30, left result at depth n-2).
+// ---------------------------------------------------------------------------
+template <bool kList>
+__device__ __forceinline__ uint32_t bot_pair(const FastPlan &P, Path &st, uint32_t (&x)[2], uint32_t Tf, uint32_t Tg,
+                                             double V0, double V1, int fr, int gl, int gbase, int L, int *sel) {
+    // x[0] = W3, x[1] = pk
+    uint32_t a = (x[1] >> 16) & 15u, b = (x[1] >> 20) & 15u;
+    double dm = 0;
+    if (kList || !(fr & 1)) dm = shfld(V0, (int)lut4(Tf, (a << 4) | b));
+    const uint32_t bl = leaf_decide<kList>(st, dm, fr & 1, gl, gbase, L, sel, x);
+    x[1] = (x[1] & ~(1u << 24)) | (bl << 24);
+    a = (x[1] >> 16) & 15u;
+    b = (x[1] >> 20) & 15u;
+    const uint32_t blin = (x[1] >> 24) & 1u;
+    if (kList || !(fr & 2)) dm = shfld(V1, (int)lut4(Tg, (blin << 8) | (a << 4) | b));
+    const uint32_t br = leaf_decide<kList>(st, dm, fr & 2, gl, gbase, L, sel, x);
+    const uint32_t bl2 = (x[1] >> 24) & 1u;
+    return (bl2 ^ br) | (br << 1);
+}
+
+template <bool kList>
+__device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem &M, const MOp &op, const int32_t *y, Path &st,
+                                        uint32_t Tf0, int gl, int gbase, int L, int *sel, int lane, int vlane) {
+    const int p0 = op.tab;
+    const int fr = op.cnt;
+    const uint32_t *ft = P.f_tab, *gt = P.g_tab;
+    const int l31 = lane & 31;
+    // tables of the 7 internal nodes (q0's f table arrives prefetched)
+    const uint32_t Tg0 = gt[(size_t)p0 * 64 + lane];
+    const int p1 = 2 * p0 + 1, p2 = 2 * p0 + 2, p3 = 4 * p0 + 3;
+    const uint32_t Tf1 = ft[(size_t)p1 * 32 + l31], Tg1 = gt[(size_t)p1 * 64 + lane];
+    const uint32_t Tf2 = ft[(size_t)p2 * 32 + l31], Tg2 = gt[(size_t)p2 * 64 + lane];
+    const uint32_t Tf3 = ft[(size_t)p3 * 32 + l31], Tg3 = gt[(size_t)p3 * 64 + lane];
+    const uint32_t Tf4 = ft[(size_t)(p3 + 1) * 32 + l31], Tg4 = gt[(size_t)(p3 + 1) * 64 + lane];
+    const uint32_t Tf5 = ft[(size_t)(p3 + 2) * 32 + l31], Tg5 = gt[(size_t)(p3 + 2) * 64 + lane];
+    const uint32_t Tf6 = ft[(size_t)(p3 + 3) * 32 + l31], Tg6 = gt[(size_t)(p3 + 3) * 64 + lane];
+    const double *vr = P.vcl + op.vrow + vlane;
+    const int v = P.v;
+    uint32_t x[2];
+    x[0] = sym_word(P, M, op, y, gbase + pfield(st.ps, op.sh_src), 0);  // W3
+    x[1] = 0;
+    // ---- q0 left: W2 = f(W3)
+    uint32_t w2 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w2 |= lut4(Tf0, (((x[0] >> (4 * i)) & 15u) << 4) | ((x[0] >> (4 * i + 16)) & 15u)) << (4 * i);
+    x[1] = w2;
+    // q1: W1 = f(W2) ; leaves 0,1 ; W1 = g(W2) ; leaves 2,3
+    uint32_t w1 = lut4(Tf1, ((w2 & 15u) << 4) | ((w2 >> 8) & 15u)) | (lut4(Tf1, (((w2 >> 4) & 15u) << 4) | ((w2 >> 12) & 15u)) << 4);
+    x[1] |= w1 << 16;
+    uint32_t c = bot_pair<kList>(P, st, x, Tf3, Tg3, vr[0], vr[v], fr, gl, gbase, L, sel);
+    x[1] = (x[1] & ~(3u << 25)) | (c << 25);
+    w2 = x[1] & 0xffffu;
+    {
+        const uint32_t c2 = (x[1] >> 25) & 3u;
+        w1 = lut4(Tg1, ((c2 & 1u) << 8) | ((w2 & 15u) << 4) | ((w2 >> 8) & 15u)) |
+             (lut4(Tg1, ((c2 >> 1) << 8) | (((w2 >> 4) & 15u) << 4) | ((w2 >> 12) & 15u)) << 4);
+    }
+    x[1] = (x[1] & ~(0xffu << 16)) | (w1 << 16);
+    c = bot_pair<kList>(P, st, x, Tf4, Tg4, vr[2 * v], vr[3 * v], fr >> 2, gl, gbase, L, sel);
+    {
+        const uint32_t c2 = (x[1] >> 25) & 3u;
+        const uint32_t c3 = (c2 ^ c) | (c << 2);  // combine at depth n-2
+        x[1] = (x[1] & ~(15u << 27)) | (c3 << 27);
+    }
+    // ---- q0 right: W2 = g(W3, c3)
+    {
+        const uint32_t c3 = (x[1] >> 27) & 15u;
+        w2 = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            w2 |= lut4(Tg0, (((c3 >> i) & 1u) << 8) | (((x[0] >> (4 * i)) & 15u) << 4) | ((x[0] >> (4 * i + 16)) & 15u))
+                  << (4 * i);
+        x[1] = (x[1] & ~0xffffu) | w2;
+    }
+    w1 = lut4(Tf2, ((w2 & 15u) << 4) | ((w2 >> 8) & 15u)) | (lut4(Tf2, (((w2 >> 4) & 15u) << 4) | ((w2 >> 12) & 15u)) << 4);
+    x[1] = (x[1] & ~(0xffu << 16)) | (w1 << 16);
+    c = bot_pair<kList>(P, st, x, Tf5, Tg5, vr[4 * v], vr[5 * v], fr >> 4, gl, gbase, L, sel);
+    x[1] = (x[1] & ~(3u << 25)) | (c << 25);
+    w2 = x[1] & 0xffffu;
+    {
+        const uint32_t c2 = (x[1] >> 25) & 3u;
+        w1 = lut4(Tg2, ((c2 & 1u) << 8) | ((w2 & 15u) << 4) | ((w2 >> 8) & 15u)) |
+             (lut4(Tg2, ((c2 >> 1) << 8) | (((w2 >> 4) & 15u) << 4) | ((w2 >> 12) & 15u)) << 4);
+    }
+    x[1] = (x[1] & ~(0xffu << 16)) | (w1 << 16);
+    c = bot_pair<kList>(P, st, x, Tf6, Tg6, vr[6 * v], vr[7 * v], fr >> 6, gl, gbase, L, sel);
+    const uint32_t c2 = (x[1] >> 25) & 3u;
+    const uint32_t c3r = (c2 ^ c) | (c << 2);
+    const uint32_t c3l = (x[1] >> 27) & 15u;
+    const uint32_t res = (c3l ^ c3r) | (c3r << 4);  // combine at depth n-3: 8 bits
+    M.st(op.flags & MF_DST_LDS, op.dst_row, lane, res);
+    if (!(op.flags & MF_TO_R)) st.pu = pset(st.pu, op.sh_dst, gl);
+}
+
 template <int KIND>
-__global__ __launch_bounds__(64) void lut_fast_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
-                                                      uint8_t *__restrict__ out) {
+__global__ __launch_bounds__(64, 6) void lut_fast_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
+                                                         uint8_t *__restrict__ out) {
     constexpr bool kList = (KIND == K_SCL_LUT || KIND == K_FASTSCL_LUT);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
     int *sel = (int *)lds_dyn;  // 64 ints of survivor-selection scratch
@@ -197,7 +338,8 @@ __global__ __launch_bounds__(64) void lut_fast_kernel(FastPlan P, const int32_t 
     const int gl = lane & (gs - 1);
     const int gbase = lane & ~(gs - 1);
     const int L = kList ? P.L : 1;
-    const int N = P.N, n = P.n;
+    const int N = P.N;
+    const int vlane = lane < P.v ? lane : 0;
     const int64_t ngroups = (B + P.fpw - 1) / P.fpw;
     const double kInf = __builtin_huge_val();
 
@@ -209,146 +351,122 @@ __global__ __launch_bounds__(64) void lut_fast_kernel(FastPlan P, const int32_t 
         const bool frame_ok = frame < B;
         if (!frame_ok) frame = B - 1;
         const int32_t *y = in + frame * (int64_t)N;
-        double pm = (gl == 0) ? 0.0 : kInf;
-        uint64_t ps = self, pu = self;
+        Path st;
+        st.pm = (gl == 0) ? 0.0 : kInf;
+        st.ps = self;
+        st.pu = self;
 
-        Op nxt = P.ops[0];
-        Pre pre = fetch_pre(P, nxt, lane);
+        MOp nxt = P.ops[0];
+        Pre pre = fetch_pre(P, nxt, lane, vlane);
         for (int oi = 0; oi < P.nops; ++oi) {
-            const Op op = nxt;
+            const MOp op = nxt;
             const Pre cur = pre;
             if (oi + 1 < P.nops) {
                 nxt = P.ops[oi + 1];
-                pre = fetch_pre(P, nxt, lane);
+                pre = fetch_pre(P, nxt, lane, vlane);
             }
-            const int d = op.d, node = op.node;
-            bool touched_glb = d < P.lds_from;
+            const int fl = op.flags;
             switch (op.type) {
+                case OP_BOT3:
+                    bot3_op<kList>(P, M, op, y, st, cur.T, gl, gbase, L, sel, lane, vlane);
+                    break;
                 case OP_F:
-                    fg_op<false>(P, M, y, d, gbase + ptr_get(ps, d), 0, cur.T, lane);
-                    ps = ptr_set(ps, d + 1, gl);
-                    touched_glb = (d + 1) < P.lds_from;
+                    fg_op<false>(P, M, op, y, gbase + pfield(st.ps, op.sh_src), 0, cur.T, lane);
+                    st.ps = pset(st.ps, op.sh_dst, gl);
                     break;
                 case OP_G:
-                    fg_op<true>(P, M, y, d, gbase + ptr_get(ps, d), gbase + ptr_get(pu, d + 1), cur.T, lane);
-                    ps = ptr_set(ps, d + 1, gl);
-                    touched_glb = (d + 1) < P.lds_from;
+                    fg_op<true>(P, M, op, y, gbase + pfield(st.ps, op.sh_src), gbase + pfield(st.pu, op.sh_u), cur.T,
+                                lane);
+                    st.ps = pset(st.ps, op.sh_dst, gl);
                     break;
                 case OP_LEAF_L:
                 case OP_LEAF_R: {
                     const bool right = op.type == OP_LEAF_R;
-                    const bool frozen = op.aux != 0;
-                    const int src = gbase + ptr_get(ps, d);
-                    uint32_t dec = 0;
+                    const bool frozen = op.cnt != 0;
+                    double dm = 0;
                     if (kList || !frozen) {
-                        uint32_t a, b;
-                        if (d == 0) {
-                            a = chan_sym(y, 0, P.v, P.err);
-                            b = chan_sym(y, 1, P.v, P.err);
-                        } else {
-                            const uint32_t W = M.ld(d >= P.lds_from, P.S_row[d], src);
-                            a = W & 15u;
-                            b = (W >> 4) & 15u;
-                        }
-                        uint32_t idx = (a << 4) | b;
-                        if (right) idx |= (M.ld(n >= P.lds_from, P.U_row[n], gbase + ptr_get(pu, n)) & 1u) << 8;
-                        const int s = (int)lut4(cur.T, idx);
-                        const double dm = shfld(cur.V, s);  // vcl[n-1][k][s] (H3)
-                        if (!kList) {
-                            dec = dm <= 0;  // H4
-                        } else if (frozen) {
-                            pm += fabs(dm) * (double)(dm < 0);
-                        } else {
-                            const double kf = pm + fabs(dm);
-                            const Sel sl = select_survivors(pm, kf, gl, gbase, L, sel);
-                            const int p = gbase + sl.parent;
-                            const uint32_t hd = dm < 0;
-                            dec = (uint32_t)__shfl((int)hd, p) ^ (sl.upper ? 1u : 0u);
-                            pm = pick(sl.upper, shfld(kf, p), shfld(pm, p));
-                            ps = shfl64(ps, p);
-                            pu = shfl64(pu, p);
-                        }
+                        const uint32_t W = sym_word(P, M, op, y, gbase + pfield(st.ps, op.sh_src), 0, 2);
+                        uint32_t idx = ((W & 15u) << 4) | ((W >> 4) & 15u);
+                        if (right) idx |= (M.ld(fl & MF_U_LDS, op.u_row, gbase + pfield(st.pu, op.sh_u)) & 1u) << 8;
+                        dm = shfld(cur.V, (int)lut4(cur.T, idx));  // vcl[n-1][k][s] (H3)
                     }
-                    const bool l = n >= P.lds_from;
-                    if (right) {
-                        M.st(l, P.R_row[n], lane, dec);
-                    } else {
-                        M.st(l, P.U_row[n], lane, dec);
-                        pu = ptr_set(pu, n, gl);
-                    }
-                    touched_glb = !l;
+                    uint32_t none[1] = {0};
+                    const uint32_t dec = leaf_decide<kList>(st, dm, frozen, gl, gbase, L, sel, none);
+                    M.st(fl & MF_DST_LDS, op.dst_row, lane, dec);
+                    if (!right) st.pu = pset(st.pu, op.sh_dst, gl);
                     break;
                 }
                 case OP_COMB: {
-                    const int ctemp = N >> (d + 1);
-                    const int usrc = gbase + ptr_get(pu, d + 1);
-                    const bool to_r = (d == 0) || (node & 1);
-                    const bool cl = (d + 1) >= P.lds_from;
+                    const int ctemp = op.cnt;
+                    const int usrc = gbase + pfield(st.pu, op.sh_u);
+                    const bool ul = fl & MF_U_LDS, rl = fl & MF_R_LDS, dl = fl & MF_DST_LDS;
                     if (ctemp < 32) {
                         const uint32_t m = (1u << ctemp) - 1u;
-                        const uint32_t ul = M.ld(cl, P.U_row[d + 1], usrc) & m;
-                        const uint32_t r = M.ld(cl, P.R_row[d + 1], lane) & m;
-                        put_node(P, M, d, to_r, 0, (ul ^ r) | (r << ctemp), lane);
+                        const uint32_t u = M.ld(ul, op.u_row, usrc) & m;
+                        const uint32_t r = M.ld(rl, op.r_row, lane) & m;
+                        M.st(dl, op.dst_row, lane, (u ^ r) | (r << ctemp));
                     } else {
                         const int cw = ctemp >> 5;
                         for (int w = 0; w < cw; ++w) {
-                            const uint32_t ul = M.ld(cl, P.U_row[d + 1] + w, usrc);
-                            const uint32_t r = M.ld(cl, P.R_row[d + 1] + w, lane);
-                            put_node(P, M, d, to_r, w, ul ^ r, lane);
-                            put_node(P, M, d, to_r, cw + w, r, lane);
+                            const uint32_t u = M.ld(ul, op.u_row + w, usrc);
+                            const uint32_t r = M.ld(rl, op.r_row + w, lane);
+                            M.st(dl, op.dst_row + w, lane, u ^ r);
+                            M.st(dl, op.dst_row + cw + w, lane, r);
                         }
                     }
-                    if (!to_r) pu = ptr_set(pu, d, gl);
-                    touched_glb = d < P.lds_from || (d + 1) < P.lds_from;
+                    if (!(fl & MF_TO_R)) st.pu = pset(st.pu, op.sh_dst, gl);
                     break;
                 }
                 default: {  // special nodes, FastSCLUT.cpp:46-107 / FastSCLLUTDecoder.cpp:82-213
-                    const int temp = N >> d;
-                    const int src = gbase + ptr_get(ps, d);
-                    const bool to_r = (node & 1);
-                    const int base_pos = temp * node;
+                    const int temp = op.cnt;
+                    const int src = gbase + pfield(st.ps, op.sh_src);
+                    const bool dl = fl & MF_DST_LDS;
                     const int nwo = (temp + 31) >> 5;
+                    const double *vq = P.vcl + (size_t)op.vrow * P.v;  // row d-1, position temp*node
+                    auto sym = [&](int j) -> int {
+                        const uint32_t w = M.ld(fl & MF_SRC_LDS, op.src_row + (j >> 3), src);
+                        return (int)((w >> ((j & 7) << 2)) & 15u);
+                    };
+                    auto llr = [&](int j) -> double { return vq[(size_t)j * P.v + sym(j)]; };
                     if (op.type == OP_R0) {
                         if (kList) {
                             for (int j = 0; j < temp; ++j) {
-                                const double l = vcl_at4(P, d - 1, base_pos + j, (int)node_sym4(P, M, y, d, src, j));
-                                pm += (double)(float)(l < 0) * fabs(l);
+                                const double l = llr(j);
+                                st.pm += (double)(float)(l < 0) * fabs(l);
                             }
                         }
-                        for (int w = 0; w < nwo; ++w) put_node(P, M, d, to_r, w, 0u, lane);
+                        for (int w = 0; w < nwo; ++w) M.st(dl, op.dst_row + w, lane, 0u);
                     } else if (op.type == OP_REP) {
                         uint32_t fill = 0;
                         if (!kList) {
                             double S = 0;
-                            for (int j = 0; j < temp; ++j)
-                                S += vcl_at4(P, d - 1, base_pos + j, (int)node_sym4(P, M, y, d, src, j));
+                            for (int j = 0; j < temp; ++j) S += llr(j);
                             fill = S <= 0 ? 0xffffffffu : 0u;
                         } else {
-                            double kk = pm, kf = pm;
+                            double kk = st.pm, kf = st.pm;
                             for (int j = 0; j < temp; ++j) {
-                                const double l = vcl_at4(P, d - 1, base_pos + j, (int)node_sym4(P, M, y, d, src, j));
+                                const double l = llr(j);
                                 kk += (double)(l < 0) * fabs(l);
                                 kf += (double)(l >= 0) * fabs(l);
                             }
                             const Sel sl = select_survivors(kk, kf, gl, gbase, L, sel);
                             const int p = gbase + sl.parent;
-                            pm = pick(sl.upper, shfld(kf, p), shfld(kk, p));
-                            ps = shfl64(ps, p);
-                            pu = shfl64(pu, p);
+                            st.pm = pick(sl.upper, shfld(kf, p), shfld(kk, p));
+                            st.ps = shfl64(st.ps, p);
+                            st.pu = shfl64(st.pu, p);
                             fill = sl.upper ? 0xffffffffu : 0u;
                         }
                         const uint32_t m = temp < 32 ? ((1u << temp) - 1u) : 0xffffffffu;
-                        for (int w = 0; w < nwo; ++w) put_node(P, M, d, to_r, w, fill & m, lane);
+                        for (int w = 0; w < nwo; ++w) M.st(dl, op.dst_row + w, lane, fill & m);
                     } else if (op.type == OP_SPC) {  // FastSC only
                         uint32_t parity = 0;
                         double best = 0;
                         int bi = 0;
-                        uint32_t bw = 0;  // word holding the first-min position
                         for (int w = 0; w < nwo; ++w) {
                             uint32_t word = 0;
                             for (int i = 0; i < 32 && 32 * w + i < temp; ++i) {
                                 const int j = 32 * w + i;
-                                const double l = vcl_at4(P, d - 1, base_pos + j, (int)node_sym4(P, M, y, d, src, j));
+                                const double l = llr(j);
                                 const uint32_t h = l <= 0;
                                 word |= h << i;
                                 parity ^= h;
@@ -358,23 +476,17 @@ __global__ __launch_bounds__(64) void lut_fast_kernel(FastPlan P, const int32_t 
                                     bi = j;
                                 }
                             }
-                            put_node(P, M, d, to_r, w, word, lane);
+                            M.st(dl, op.dst_row + w, lane, word);
                         }
                         if (parity) {
-                            const bool l = d >= P.lds_from;
-                            const int row = (to_r ? P.R_row[d] : P.U_row[d]) + (bi >> 5);
-                            bw = M.ld(l, row, lane) ^ (1u << (bi & 31));
-                            M.st(l, row, lane, bw);
+                            const int row = op.dst_row + (bi >> 5);
+                            M.st(dl, row, lane, M.ld(dl, row, lane) ^ (1u << (bi & 31)));
                         }
                     } else if (!kList) {  // OP_R1, FastSC: `<= 0`
                         for (int w = 0; w < nwo; ++w) {
                             uint32_t word = 0;
-                            for (int i = 0; i < 32 && 32 * w + i < temp; ++i) {
-                                const int j = 32 * w + i;
-                                const double l = vcl_at4(P, d - 1, base_pos + j, (int)node_sym4(P, M, y, d, src, j));
-                                word |= (uint32_t)(l <= 0) << i;
-                            }
-                            put_node(P, M, d, to_r, w, word, lane);
+                            for (int i = 0; i < 32 && 32 * w + i < temp; ++i) word |= (uint32_t)(llr(32 * w + i) <= 0) << i;
+                            M.st(dl, op.dst_row + w, lane, word);
                         }
                     } else if constexpr (KIND == K_FASTSCL_LUT) {  // OP_R1, FastSCL: :99-166
                         const int m = (L - 1) < temp ? (L - 1) : temp;
@@ -383,7 +495,7 @@ __global__ __launch_bounds__(64) void lut_fast_kernel(FastPlan P, const int32_t 
                             uint32_t word = 0;
                             for (int i = 0; i < 32 && 32 * w + i < temp; ++i) {
                                 const int j = 32 * w + i;
-                                const double l = vcl_at4(P, d - 1, base_pos + j, (int)node_sym4(P, M, y, d, src, j));
+                                const double l = llr(j);
                                 word |= (uint32_t)(l < 0) << i;
                                 ((double *)(g + (size_t)(P.K_row + 2 * j) * 64))[lane] = fabs(l);
                             }
@@ -435,13 +547,13 @@ __global__ __launch_bounds__(64) void lut_fast_kernel(FastPlan P, const int32_t 
 #pragma unroll
                         for (int layer = 0; layer < kMaxM; ++layer) {
                             if (layer < m) {
-                                const double kf = pm + ms[layer];
-                                const Sel sl = select_survivors(pm, kf, gl, gbase, L, sel);
+                                const double kf = st.pm + ms[layer];
+                                const Sel sl = select_survivors(st.pm, kf, gl, gbase, L, sel);
                                 const int p = gbase + sl.parent;
                                 const int pos_old = ord[layer];  // H2
-                                pm = pick(sl.upper, shfld(kf, p), shfld(pm, p));
-                                ps = shfl64(ps, p);
-                                pu = shfl64(pu, p);
+                                st.pm = pick(sl.upper, shfld(kf, p), shfld(st.pm, p));
+                                st.ps = shfl64(st.ps, p);
+                                st.pu = shfl64(st.pu, p);
                                 origin = __shfl(origin, p);
 #pragma unroll
                                 for (int q = 0; q < kMaxM; ++q) {
@@ -458,20 +570,19 @@ __global__ __launch_bounds__(64) void lut_fast_kernel(FastPlan P, const int32_t 
                             for (int q = 0; q < kMaxM; ++q)
                                 if (q < m && flip[q] >= 0 && (flip[q] >> 5) == w) word ^= 1u << (flip[q] & 31);
                             if (temp < 32) word &= (1u << temp) - 1u;
-                            put_node(P, M, d, to_r, w, word, lane);
+                            M.st(dl, op.dst_row + w, lane, word);
                         }
-                        touched_glb = true;
                     }
-                    if (!to_r) pu = ptr_set(pu, d, gl);
+                    if (!(fl & MF_TO_R)) st.pu = pset(st.pu, op.sh_dst, gl);
                     break;
                 }
             }
-            if (touched_glb) wave_sync();  // drain global writes before any cross-lane read
+            if (fl & MF_SYNC) wave_sync();  // drain global writes before any cross-lane read
         }
 
         // Root partial sums -> u = x F^{(x)n} (FastSCLUT.cpp:186-198), R[0] rows.
-        const bool rl = 0 >= P.lds_from;
-        const int r0 = P.R_row[0];
+        const bool rl = P.R0_lds;
+        const int r0 = P.R0_row;
         const int nwr = (N + 31) >> 5;
         for (int w = 0; w < nwr; ++w) {
             uint32_t x = M.ld(rl, r0 + w, lane);
@@ -490,9 +601,9 @@ __global__ __launch_bounds__(64) void lut_fast_kernel(FastPlan P, const int32_t 
         wave_sync();
         int best = 0;
         if (kList) {
-            double bpm = shfld(pm, gbase);
+            double bpm = shfld(st.pm, gbase);
             for (int j = 1; j < L; ++j) {
-                const double pj = shfld(pm, gbase + j);
+                const double pj = shfld(st.pm, gbase + j);
                 if (pj < bpm) {
                     bpm = pj;
                     best = j;
