@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--N", type=int, default=1024)
     ap.add_argument("--K", type=int, default=512)
     ap.add_argument("--L", type=int, default=8)
-    ap.add_argument("--frames", type=int, default=1 << 16, help="frames per GPU per step")
+    ap.add_argument("--frames", type=int, default=1 << 18, help="frames per GPU per step")
     ap.add_argument("--ebn0", type=float, default=2.0)
     ap.add_argument("--max-waves", type=int, default=0)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
@@ -50,17 +50,27 @@ def parse():
     return ap.parse_args()
 
 
-def synth_frames(N, K, frames, ebn0, seed, msgbits, v=16, delta=0.5):
-    """Reference driver channel (mainQuantizedDecoder_LLRDomain.py:132-176) with a
-    uniform channel quantizer matching the synthetic min-sum tables."""
-    from quantized_decoder_polar_codes_amd import codes as C
+def synth_frames(N, K, frames, ebn0, seed, msgbits, dev, v=16, delta=0.5):
+    """Reference driver channel (mainQuantizedDecoder_LLRDomain.py:132-176), generated
+    on the GPU with torch's counter-based RNG: message bits, polar encoding
+    (x = u F^{(x)n}, the un-vendored PolarEnc restated), BPSK, AWGN at Eb/N0,
+    LLR = 2y/sigma^2 and a uniform 16-level channel quantizer matching the
+    synthetic min-sum tables.  Returns device tensors (msg uint8 [F,K], sym int32 [F,N])."""
+    import torch
 
-    rng = np.random.default_rng(seed)
-    sigma = np.sqrt(1 / (2 * (K / N) * 10 ** (ebn0 / 10)))
-    msg = rng.integers(0, 2, size=(frames, K), dtype=np.uint8)
-    x = C.polar_encode(msg, msgbits, N)
-    llr = ((1.0 - 2.0 * x) + rng.normal(0, sigma, size=(frames, N)).astype(np.float32)) * (2 / sigma ** 2)
-    sym = np.clip(np.rint(llr / delta + (v - 1) / 2.0), 0, v - 1).astype(np.int32)
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    sigma = float(np.sqrt(1 / (2 * (K / N) * 10 ** (ebn0 / 10))))
+    msg = torch.randint(0, 2, (frames, K), generator=g, device=dev, dtype=torch.uint8)
+    u = torch.zeros((frames, N), dtype=torch.uint8, device=dev)
+    u[:, torch.as_tensor(msgbits, device=dev)] = msg
+    m = 1
+    while m < N:
+        w = u.view(frames, N // (2 * m), 2, m)
+        w[:, :, 0, :] ^= w[:, :, 1, :]
+        m *= 2
+    llr = (1.0 - 2.0 * u.float() + sigma * torch.randn((frames, N), generator=g, device=dev)) * (2 / sigma ** 2)
+    sym = torch.clamp(torch.round(llr / delta + (v - 1) / 2.0), 0, v - 1).to(torch.int32)
     return msg, sym
 
 
@@ -125,9 +135,7 @@ def main():
                         engine=args.engine)
     info = dec.info()
     # rank r owns global frames [r*F, (r+1)*F): seed by rank -> disjoint frame sets
-    msg, sym = synth_frames(N, K, args.frames, args.ebn0, 1234 + rank, mb)
-    d_sym = torch.from_numpy(sym).to(dev)
-    d_msg = torch.from_numpy(msg).to(dev)
+    d_msg, d_sym = synth_frames(N, K, args.frames, args.ebn0, 1234 + rank, mb, dev)
     stream = torch.cuda.current_stream(dev)
 
     out = None
@@ -189,7 +197,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic: seeded AWGN frames (BPSK, Eb/N0 dB below), uniform 16-level channel quantizer, "
+            "data": "synthetic, generated on the GPU (torch Philox): random messages, polar-encoded, BPSK + AWGN at Eb/N0 below, uniform 16-level channel quantizer, "
                     "synthetic saturating min-sum 16-level LUTs; resident in HBM",
             "config": {"workload": f"{args.kind} N={N} K={K} L={L} Q=16 (5G-NR PW code, no CRC)",
                        "decoder": args.kind, "N": N, "K": K, "L": L, "v": 16, "frames_per_gpu_per_step": args.frames,
@@ -207,7 +215,8 @@ def main():
                                               "bytes_per_frame": LOOKUPS_PER_FRAME * ONCHIP_BYTES_PER_LOOKUP}},
         }
         if world == 1 and not args.no_cpu_baseline:
-            cb, ref_out = cpu_baseline(args, packed, fm, nt, sym, args.cpu_baseline_seconds)
+            sample = d_sym[:4096].cpu().numpy()
+            cb, ref_out = cpu_baseline(args, packed, fm, nt, sample, args.cpu_baseline_seconds)
             res["cpu_baseline"] = cb
             gpu_out = out[: len(ref_out)].cpu().numpy()
             res["parity_sample"] = {"frames": int(len(ref_out)),
