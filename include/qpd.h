@@ -120,6 +120,26 @@ int qpd_decode_f64_host(qpd_decoder *dec, const double *h_llr, int64_t B, uint8_
  * check saw a channel symbol outside [0, v); synchronizes the device. */
 int qpd_check_input_error(qpd_decoder *dec);
 
+/*
+ * GPU-resident Monte-Carlo frames (replaces the driver loop
+ * mainQuantizedDecoder_LLRDomain.py:151-176): for global frame ids
+ * [frame0, frame0+B): message bits, polar encoding (x = u F^{(x)n}, natural
+ * order), BPSK, AWGN (std sigma), LLR = 2y/sigma^2 and the driver's channel
+ * quantizer (<= edges[0] -> 0, >= edges[M] -> q-1, else
+ * lut[bisect_left(edges[:M], llr) - 1]).  Random numbers are Philox4x32-10 of
+ * (seed, global frame id), so frames do not depend on batching or sharding.
+ * d_msg: device uint8 [B][K]; d_symbols: device int32 [B][N].
+ */
+typedef struct qpd_mc_channel {
+    double sigma;           /* AWGN standard deviation                 */
+    int32_t q;              /* number of channel symbols               */
+    int32_t n_edges;        /* M+1, 2..257                             */
+    const double *edges;    /* host [n_edges], ascending               */
+    const int32_t *lut;     /* host [n_edges-1], values in [0, q)      */
+} qpd_mc_channel;
+int qpd_mc_frames(qpd_decoder *dec, const qpd_mc_channel *ch, uint64_t seed, int64_t frame0, int64_t B,
+                  uint8_t *d_msg, int32_t *d_symbols, void *stream);
+
 /* Introspection for tests / benchmarks. */
 typedef struct qpd_info {
     int32_t kind, N, K, L, v;

@@ -28,6 +28,7 @@ EXPORTED = (
     "qpd_decode_f64_host",
     "qpd_check_input_error",
     "qpd_get_info",
+    "qpd_mc_frames",
 )
 
 _P = ctypes.c_void_p
@@ -57,6 +58,16 @@ class QpdConfig(ctypes.Structure):
         ("device", _i32),
         ("max_waves", _i32),
         ("engine", _i32),
+    ]
+
+
+class QpdMcChannel(ctypes.Structure):
+    _fields_ = [
+        ("sigma", ctypes.c_double),
+        ("q", _i32),
+        ("n_edges", _i32),
+        ("edges", _P),
+        ("lut", _P),
     ]
 
 
@@ -123,6 +134,8 @@ def load():
     L.qpd_check_input_error.restype = ctypes.c_int
     L.qpd_get_info.argtypes = [_P, ctypes.POINTER(QpdInfo)]
     L.qpd_get_info.restype = ctypes.c_int
+    L.qpd_mc_frames.argtypes = [_P, ctypes.POINTER(QpdMcChannel), ctypes.c_uint64, _i64, _i64, _P, _P, _P]
+    L.qpd_mc_frames.restype = ctypes.c_int
     if L.qpd_abi_version() != 1:
         raise ImportError("libqpd.so ABI version mismatch")
     _lib = L

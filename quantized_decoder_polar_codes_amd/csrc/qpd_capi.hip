@@ -13,6 +13,7 @@
 #include "qpd.h"
 #include "qpd_generic.hip"
 #include "qpd_fast.hip"
+#include "qpd_mc.hip"
 
 namespace {
 
@@ -679,6 +680,41 @@ int qpd_decode_f64_host(qpd_decoder *d, const double *h_llr, int64_t B, uint8_t 
     if ((rc = qpd_decode_f64(d, (const double *)d->h_in.p, B, (uint8_t *)d->h_out.p, nullptr))) return rc;
     if (out_b) QPD_HIP(hipMemcpy(h_out, d->h_out.p, out_b, hipMemcpyDeviceToHost));
     QPD_HIP(hipDeviceSynchronize());
+    return QPD_OK;
+}
+
+int qpd_mc_frames(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64_t frame0, int64_t B, uint8_t *d_msg,
+                  int32_t *d_symbols, void *stream) {
+    if (!d || !ch) return fail(QPD_E_INVALID, "null argument");
+    if (B < 0 || frame0 < 0) return fail(QPD_E_INVALID, "negative frame range");
+    if (B == 0) return QPD_OK;
+    if (!d_msg || !d_symbols) return fail(QPD_E_INVALID, "null buffer");
+    if (ch->n_edges < 2 || ch->n_edges > qpd::kMcMaxEdges) return fail(QPD_E_INVALID, "n_edges must be in [2, 257]");
+    if (!ch->edges || !ch->lut) return fail(QPD_E_INVALID, "null channel quantizer");
+    if (!(ch->sigma > 0) || ch->q < 2) return fail(QPD_E_INVALID, "sigma must be > 0 and q >= 2");
+    for (int i = 0; i + 1 < ch->n_edges; ++i) {
+        if (!(ch->edges[i] <= ch->edges[i + 1])) return fail(QPD_E_INVALID, "edges must be ascending");
+        if (ch->lut[i] < 0 || ch->lut[i] >= ch->q) return fail(QPD_E_INVALID, "lut entry outside [0, q)");
+    }
+    int rc = set_device(d);
+    if (rc) return rc;
+    qpd::McChannel C;
+    std::memset(&C, 0, sizeof(C));
+    C.N = d->N;
+    C.K = d->K;
+    C.q = ch->q;
+    C.n_edges = ch->n_edges;
+    C.seed_lo = (uint32_t)seed;
+    C.seed_hi = (uint32_t)(seed >> 32);
+    C.sigma = (float)ch->sigma;
+    C.llr_scale = (float)(2.0 / (ch->sigma * ch->sigma));
+    C.info_pos = (const int32_t *)d->info_pos.p;
+    for (int i = 0; i < ch->n_edges; ++i) C.edges[i] = ch->edges[i];
+    for (int i = 0; i + 1 < ch->n_edges; ++i) C.lut[i] = ch->lut[i];
+    const int grid = (int)std::min<int64_t>(B, 256 * 16);
+    hipLaunchKernelGGL(qpd::mc_frames_kernel, dim3(grid), dim3(64), (size_t)d->N, (hipStream_t)stream, C, frame0, B,
+                       d_msg, d_symbols);
+    QPD_HIP(hipGetLastError());
     return QPD_OK;
 }
 
