@@ -575,18 +575,20 @@ int qpd_decode(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_o
         const int64_t rounds = (fgroups + fgrid - 1) / fgrid;
         fgrid = (int)((fgroups + rounds - 1) / rounds);
         const size_t lds = (size_t)d->lds_bytes;
+        qpd::FastPlan fp = d->fplan;
+        fp.in_vec = ((uintptr_t)d_symbols & 15u) == 0 && (fp.N & 3) == 0;
         switch (d->kind) {
             case QPD_SC_LUT:
-                hipLaunchKernelGGL(qpd::lut_fast_kernel<qpd::K_SC_LUT>, dim3(fgrid), dim3(64), lds, st, d->fplan, d_symbols, B, d_out);
+                hipLaunchKernelGGL(qpd::lut_fast_kernel<qpd::K_SC_LUT>, dim3(fgrid), dim3(64), lds, st, fp, d_symbols, B, d_out);
                 break;
             case QPD_SCL_LUT:
-                hipLaunchKernelGGL(qpd::lut_fast_kernel<qpd::K_SCL_LUT>, dim3(fgrid), dim3(64), lds, st, d->fplan, d_symbols, B, d_out);
+                hipLaunchKernelGGL(qpd::lut_fast_kernel<qpd::K_SCL_LUT>, dim3(fgrid), dim3(64), lds, st, fp, d_symbols, B, d_out);
                 break;
             case QPD_FASTSC_LUT:
-                hipLaunchKernelGGL(qpd::lut_fast_kernel<qpd::K_FASTSC_LUT>, dim3(fgrid), dim3(64), lds, st, d->fplan, d_symbols, B, d_out);
+                hipLaunchKernelGGL(qpd::lut_fast_kernel<qpd::K_FASTSC_LUT>, dim3(fgrid), dim3(64), lds, st, fp, d_symbols, B, d_out);
                 break;
             case QPD_FASTSCL_LUT:
-                hipLaunchKernelGGL(qpd::lut_fast_kernel<qpd::K_FASTSCL_LUT>, dim3(fgrid), dim3(64), lds, st, d->fplan, d_symbols, B, d_out);
+                hipLaunchKernelGGL(qpd::lut_fast_kernel<qpd::K_FASTSCL_LUT>, dim3(fgrid), dim3(64), lds, st, fp, d_symbols, B, d_out);
                 break;
             default:
                 return fail(QPD_E_INVALID, "bad kind");
@@ -718,4 +720,15 @@ int qpd_mc_frames(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64
     return QPD_OK;
 }
 
+#ifdef QPD_STAMPS
+// Diagnostic builds only (not declared in qpd.h): read and clear the per-class
+// cycle / count accumulators of lut_fast_kernel.
+int qpd_debug_stamps(unsigned long long *out64) {
+    QPD_HIP(hipDeviceSynchronize());
+    QPD_HIP(hipMemcpyFromSymbol(out64, HIP_SYMBOL(qpd::qpd_stamp_acc), 64 * sizeof(unsigned long long)));
+    static const unsigned long long zero[64] = {0};
+    QPD_HIP(hipMemcpyToSymbol(HIP_SYMBOL(qpd::qpd_stamp_acc), zero, sizeof(zero)));
+    return QPD_OK;
+}
+#endif
 }  // extern "C"

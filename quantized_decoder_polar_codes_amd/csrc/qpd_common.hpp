@@ -76,8 +76,66 @@ struct Sel {
     bool upper;  // candidate came from the second half (flip / penalty branch)
 };
 
+// Group-of-8 exchange by DPP (VALU, no LDS round trip): partner m (1..7) of
+// lane i is lane i^m.  quad_perm gives XOR 1/2/3, row_half_mirror XOR 7, and
+// their composition XOR 4/5/6.
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppXor3 = 0x1B, kDppHalfMirror = 0x141;
+
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t x) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <int M>
+__device__ __forceinline__ uint64_t xor_lane8(uint64_t x, uint64_t hm) {  // hm = x of lane i^7
+    if constexpr (M == 1) return dpp64<kDppXor1>(x);
+    if constexpr (M == 2) return dpp64<kDppXor2>(x);
+    if constexpr (M == 3) return dpp64<kDppXor3>(x);
+    if constexpr (M == 4) return dpp64<kDppXor3>(hm);
+    if constexpr (M == 5) return dpp64<kDppXor2>(hm);
+    if constexpr (M == 6) return dpp64<kDppXor1>(hm);
+    return hm;
+}
+
+// Rank contribution of partner gl^M.  Keys are non-negative doubles (or +inf),
+// so their order is the order of their bit patterns as unsigned integers.
+// The candidate-index tie break (partner j < gl) holds iff gl has the highest
+// bit of M set.
+template <int M>
+__device__ __forceinline__ void rank8_partner(uint64_t K, uint64_t F, uint64_t hk, uint64_t hf, int gl, int &rk,
+                                              int &rf) {
+    constexpr int hb = M >= 4 ? 2 : (M >= 2 ? 1 : 0);
+    const bool t = (gl >> hb) & 1;
+    const uint64_t ok = xor_lane8<M>(K, hk), of = xor_lane8<M>(F, hf);
+    rk += (ok < K) | (t & (ok == K));
+    rk += of < K;
+    rf += ok <= F;
+    rf += (of < F) | (t & (of == F));
+    __builtin_amdgcn_sched_barrier(0);  // one partner at a time: bounds live temporaries
+}
+
 __device__ __forceinline__ Sel select_survivors(double kk, double kf, int gl, int gbase, int L, int *sel) {
+#ifdef QPD_EXP_NOSEL  // timing experiment only: wrong results
+    if (L > 0) return Sel{gl, false};
+#endif
     int rk = 0, rf = 0;
+#ifndef QPD_NO_DPP_SEL
+    if (L == 8) {  // lane group of 8: all partners through DPP
+        const uint64_t K = __builtin_bit_cast(uint64_t, kk), F = __builtin_bit_cast(uint64_t, kf);
+        const uint64_t hk = dpp64<kDppHalfMirror>(K), hf = dpp64<kDppHalfMirror>(F);
+        rk = F < K;
+        rf = K <= F;
+        rank8_partner<1>(K, F, hk, hf, gl, rk, rf);
+        rank8_partner<2>(K, F, hk, hf, gl, rk, rf);
+        rank8_partner<3>(K, F, hk, hf, gl, rk, rf);
+        rank8_partner<4>(K, F, hk, hf, gl, rk, rf);
+        rank8_partner<5>(K, F, hk, hf, gl, rk, rf);
+        rank8_partner<6>(K, F, hk, hf, gl, rk, rf);
+        rank8_partner<7>(K, F, hk, hf, gl, rk, rf);
+    } else
+#endif
     for (int j = 0; j < L; ++j) {
         const double ok = shfld(kk, gbase + j);
         const double of = shfld(kf, gbase + j);

@@ -59,6 +59,7 @@ struct MOp {
 
 struct FastPlan {
     int32_t N, n, K, L, v, gs, fpw, nops, max_r1;
+    int32_t in_vec;               // per launch: input rows are 16-byte aligned
     int32_t lds_rows, glb_rows, lds_from;
     int32_t R0_row, R0_lds;      // root partial sums (R[0])
     int32_t H_row, K_row, I_row;  // R1 scratch (global)
@@ -116,35 +117,82 @@ __device__ __forceinline__ uint32_t chan_word(const int32_t *y, int e0, int cnt,
     return w;
 }
 
+// Eight channel symbols e0..e0+7 as one nibble word; `vec` = the input rows
+// are 16-byte aligned (two 128-bit loads instead of eight 32-bit ones).
+__device__ __forceinline__ uint32_t chan_word8(const int32_t *y, int e0, bool vec, int v, int32_t *err) {
+    if (!vec) return chan_word(y, e0, 8, v, err);
+    const int4 a = *(const int4 *)(y + e0), b = *(const int4 *)(y + e0 + 4);
+    const int e[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t w = 0, bad = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t s = (uint32_t)e[i];
+        bad |= s >= (uint32_t)v;
+        w |= (s >= (uint32_t)v ? 0u : s) << (4 * i);
+    }
+    if (bad) atomicOr(err, 1);
+    return w;
+}
+
 // Word w (8 symbols) of S[d] of the path whose slot is `src`.
 __device__ __forceinline__ uint32_t sym_word(const FastPlan &P, const Mem &M, const MOp &op, const int32_t *y, int src,
                                              int w, int cnt = 8) {
-    if (op.flags & MF_CHAN) return chan_word(y, 8 * w, cnt, P.v, P.err);
+    if (op.flags & MF_CHAN) return cnt == 8 ? chan_word8(y, 8 * w, P.in_vec, P.v, P.err) : chan_word(y, 8 * w, cnt, P.v, P.err);
     return M.ld(op.flags & MF_SRC_LDS, op.src_row + w, src);
 }
 
+template <bool ISG>
+__device__ __forceinline__ uint32_t fg_word(uint32_t T, uint32_t A, uint32_t B, uint32_t ub) {
+    uint32_t out = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint32_t idx = (((A >> (4 * i)) & 15u) << 4) | ((B >> (4 * i)) & 15u);
+        if (ISG) idx |= (ub >> i) & 256u;
+        out |= lut4(T, idx) << (4 * i);
+    }
+    return out;
+}
+
 // f / g op (SCLLUTDecoder.cpp:83-89 / :157-164): child symbols at depth d+1.
+// Words are processed in chunks of up to 8 whose loads are all issued before
+// the first lookup: the shallow levels live in the global slab, and one HBM
+// round trip per chunk instead of per word is what bounds these ops.
 template <bool ISG>
 __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem &M, const MOp &op, const int32_t *y, int src,
                                       int usrc, uint32_t T, int lane) {
     const int ctemp = op.cnt;
     const bool dl = op.flags & MF_DST_LDS, ul = op.flags & MF_U_LDS;
-    if (ctemp >= 8) {
-        const int nwo = ctemp >> 3;
-        for (int w = 0; w < nwo; ++w) {
-            const uint32_t A = sym_word(P, M, op, y, src, w);
-            const uint32_t B = sym_word(P, M, op, y, src, nwo + w);
-            uint32_t ub = 0;
-            if (ISG) ub = (M.ld(ul, op.u_row + (w >> 2), usrc) >> ((w & 3) << 3)) << 8;
-            uint32_t out = 0;
+    if (ctemp >= 64) {
+        const int nwo = ctemp >> 3;  // multiple of 8
+        for (int w0 = 0; w0 < nwo; w0 += 8) {
+            uint32_t A[8], B[8], ub[2] = {0u, 0u};
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                uint32_t idx = (((A >> (4 * i)) & 15u) << 4) | ((B >> (4 * i)) & 15u);
-                if (ISG) idx |= (ub >> i) & 256u;
-                out |= lut4(T, idx) << (4 * i);
+            for (int k = 0; k < 8; ++k) {
+                A[k] = sym_word(P, M, op, y, src, w0 + k);
+                B[k] = sym_word(P, M, op, y, src, nwo + w0 + k);
             }
-            M.st(dl, op.dst_row + w, lane, out);
+            if (ISG) {
+                ub[0] = M.ld(ul, op.u_row + (w0 >> 2), usrc);
+                ub[1] = M.ld(ul, op.u_row + (w0 >> 2) + 1, usrc);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                M.st(dl, op.dst_row + w0 + k, lane, fg_word<ISG>(T, A[k], B[k], ((ub[k >> 2] >> ((k & 3) << 3)) << 8)));
         }
+    } else if (ctemp >= 8) {
+        const int nwo = ctemp >> 3;  // 1, 2 or 4
+        uint32_t A[4] = {0u, 0u, 0u, 0u}, B[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k < nwo) {
+                A[k] = sym_word(P, M, op, y, src, k);
+                B[k] = sym_word(P, M, op, y, src, nwo + k);
+            }
+        }
+        const uint32_t ub = ISG ? M.ld(ul, op.u_row, usrc) : 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (k < nwo) M.st(dl, op.dst_row + k, lane, fg_word<ISG>(T, A[k], B[k], (ub >> (k << 3)) << 8));
     } else {  // ctemp in {2, 4}: the whole depth-d node (a then b) is one word
         const uint32_t W = sym_word(P, M, op, y, src, 0, 2 * ctemp);
         const uint32_t ub = ISG ? M.ld(ul, op.u_row, usrc) : 0u;
@@ -233,18 +281,18 @@ __device__ __forceinline__ uint32_t leaf_decide(Path &st, double dm, bool frozen
 // | c3 (bits 27-30, left result at depth n-2).
 // ---------------------------------------------------------------------------
 template <bool kList>
-__device__ __forceinline__ uint32_t bot_pair(const FastPlan &P, Path &st, uint32_t (&x)[2], uint32_t Tf, uint32_t Tg,
-                                             double V0, double V1, int fr, int gl, int gbase, int L, int *sel) {
+__device__ __forceinline__ uint32_t bot_pair(const FastPlan &P, Path &st, uint32_t (&x)[2], uint32_t Tf, int fo,
+                                             uint32_t Tg, double V, int vo, int fr, int gl, int gbase, int L, int *sel) {
     // x[0] = W3, x[1] = pk
     uint32_t a = (x[1] >> 16) & 15u, b = (x[1] >> 20) & 15u;
     double dm = 0;
-    if (kList || !(fr & 1)) dm = shfld(V0, (int)lut4(Tf, (a << 4) | b));
+    if (kList || !(fr & 1)) dm = shfld(V, vo + (int)lut4(Tf, ((a << 4) | b) + fo));
     const uint32_t bl = leaf_decide<kList>(st, dm, fr & 1, gl, gbase, L, sel, x);
     x[1] = (x[1] & ~(1u << 24)) | (bl << 24);
     a = (x[1] >> 16) & 15u;
     b = (x[1] >> 20) & 15u;
     const uint32_t blin = (x[1] >> 24) & 1u;
-    if (kList || !(fr & 2)) dm = shfld(V1, (int)lut4(Tg, (blin << 8) | (a << 4) | b));
+    if (kList || !(fr & 2)) dm = shfld(V, vo + 16 + (int)lut4(Tg, (blin << 8) | (a << 4) | b));
     const uint32_t br = leaf_decide<kList>(st, dm, fr & 2, gl, gbase, L, sel, x);
     const uint32_t bl2 = (x[1] >> 24) & 1u;
     return (bl2 ^ br) | (br << 1);
@@ -256,18 +304,23 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem &M, const M
     const int p0 = op.tab;
     const int fr = op.cnt;
     const uint32_t *ft = P.f_tab, *gt = P.g_tab;
-    const int l31 = lane & 31;
-    // tables of the 7 internal nodes (q0's f table arrives prefetched)
+    // Tables of the 7 internal nodes (q0's f table arrives prefetched).  Two
+    // 32-dword f tables share one register (lanes 0-31 | 32-63: p and p+1 are
+    // adjacent), addressed by adding 256 to the nibble index of the second.
     const uint32_t Tg0 = gt[(size_t)p0 * 64 + lane];
-    const int p1 = 2 * p0 + 1, p2 = 2 * p0 + 2, p3 = 4 * p0 + 3;
-    const uint32_t Tf1 = ft[(size_t)p1 * 32 + l31], Tg1 = gt[(size_t)p1 * 64 + lane];
-    const uint32_t Tf2 = ft[(size_t)p2 * 32 + l31], Tg2 = gt[(size_t)p2 * 64 + lane];
-    const uint32_t Tf3 = ft[(size_t)p3 * 32 + l31], Tg3 = gt[(size_t)p3 * 64 + lane];
-    const uint32_t Tf4 = ft[(size_t)(p3 + 1) * 32 + l31], Tg4 = gt[(size_t)(p3 + 1) * 64 + lane];
-    const uint32_t Tf5 = ft[(size_t)(p3 + 2) * 32 + l31], Tg5 = gt[(size_t)(p3 + 2) * 64 + lane];
-    const uint32_t Tf6 = ft[(size_t)(p3 + 3) * 32 + l31], Tg6 = gt[(size_t)(p3 + 3) * 64 + lane];
-    const double *vr = P.vcl + op.vrow + vlane;
+    const int p1 = 2 * p0 + 1, p3 = 4 * p0 + 3;
+    const uint32_t Tf12 = ft[(size_t)p1 * 32 + lane], Tg1 = gt[(size_t)p1 * 64 + lane], Tg2 = gt[(size_t)(p1 + 1) * 64 + lane];
+    const uint32_t Tf34 = ft[(size_t)p3 * 32 + lane], Tg3 = gt[(size_t)p3 * 64 + lane], Tg4 = gt[(size_t)(p3 + 1) * 64 + lane];
+    const uint32_t Tf56 = ft[(size_t)(p3 + 2) * 32 + lane], Tg5 = gt[(size_t)(p3 + 2) * 64 + lane],
+                   Tg6 = gt[(size_t)(p3 + 3) * 64 + lane];
+    // Leaf quanta vcl[n-1][8*node + j][s] of the 8 leaves, four leaves per
+    // register: lane 16*jj + s holds leaf 4*h + jj (v <= 16).
     const int v = P.v;
+    const int s16 = lane & 15, j16 = lane >> 4;
+    const double *vb = P.vcl + op.vrow;
+    const double Vlo = s16 < v ? vb[j16 * v + s16] : 0.0;
+    const double Vhi = s16 < v ? vb[(4 + j16) * v + s16] : 0.0;
+    (void)vlane;
     uint32_t x[2];
     x[0] = sym_word(P, M, op, y, gbase + pfield(st.ps, op.sh_src), 0);  // W3
     x[1] = 0;
@@ -277,9 +330,9 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem &M, const M
     for (int i = 0; i < 4; ++i) w2 |= lut4(Tf0, (((x[0] >> (4 * i)) & 15u) << 4) | ((x[0] >> (4 * i + 16)) & 15u)) << (4 * i);
     x[1] = w2;
     // q1: W1 = f(W2) ; leaves 0,1 ; W1 = g(W2) ; leaves 2,3
-    uint32_t w1 = lut4(Tf1, ((w2 & 15u) << 4) | ((w2 >> 8) & 15u)) | (lut4(Tf1, (((w2 >> 4) & 15u) << 4) | ((w2 >> 12) & 15u)) << 4);
+    uint32_t w1 = lut4(Tf12, ((w2 & 15u) << 4) | ((w2 >> 8) & 15u)) | (lut4(Tf12, (((w2 >> 4) & 15u) << 4) | ((w2 >> 12) & 15u)) << 4);
     x[1] |= w1 << 16;
-    uint32_t c = bot_pair<kList>(P, st, x, Tf3, Tg3, vr[0], vr[v], fr, gl, gbase, L, sel);
+    uint32_t c = bot_pair<kList>(P, st, x, Tf34, 0, Tg3, Vlo, 0, fr, gl, gbase, L, sel);
     x[1] = (x[1] & ~(3u << 25)) | (c << 25);
     w2 = x[1] & 0xffffu;
     {
@@ -288,7 +341,7 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem &M, const M
              (lut4(Tg1, ((c2 >> 1) << 8) | (((w2 >> 4) & 15u) << 4) | ((w2 >> 12) & 15u)) << 4);
     }
     x[1] = (x[1] & ~(0xffu << 16)) | (w1 << 16);
-    c = bot_pair<kList>(P, st, x, Tf4, Tg4, vr[2 * v], vr[3 * v], fr >> 2, gl, gbase, L, sel);
+    c = bot_pair<kList>(P, st, x, Tf34, 256, Tg4, Vlo, 32, fr >> 2, gl, gbase, L, sel);
     {
         const uint32_t c2 = (x[1] >> 25) & 3u;
         const uint32_t c3 = (c2 ^ c) | (c << 2);  // combine at depth n-2
@@ -304,9 +357,10 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem &M, const M
                   << (4 * i);
         x[1] = (x[1] & ~0xffffu) | w2;
     }
-    w1 = lut4(Tf2, ((w2 & 15u) << 4) | ((w2 >> 8) & 15u)) | (lut4(Tf2, (((w2 >> 4) & 15u) << 4) | ((w2 >> 12) & 15u)) << 4);
+    w1 = lut4(Tf12, 256 + (((w2 & 15u) << 4) | ((w2 >> 8) & 15u))) |
+         (lut4(Tf12, 256 + ((((w2 >> 4) & 15u) << 4) | ((w2 >> 12) & 15u))) << 4);
     x[1] = (x[1] & ~(0xffu << 16)) | (w1 << 16);
-    c = bot_pair<kList>(P, st, x, Tf5, Tg5, vr[4 * v], vr[5 * v], fr >> 4, gl, gbase, L, sel);
+    c = bot_pair<kList>(P, st, x, Tf56, 0, Tg5, Vhi, 0, fr >> 4, gl, gbase, L, sel);
     x[1] = (x[1] & ~(3u << 25)) | (c << 25);
     w2 = x[1] & 0xffffu;
     {
@@ -315,7 +369,7 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem &M, const M
              (lut4(Tg2, ((c2 >> 1) << 8) | (((w2 >> 4) & 15u) << 4) | ((w2 >> 12) & 15u)) << 4);
     }
     x[1] = (x[1] & ~(0xffu << 16)) | (w1 << 16);
-    c = bot_pair<kList>(P, st, x, Tf6, Tg6, vr[6 * v], vr[7 * v], fr >> 6, gl, gbase, L, sel);
+    c = bot_pair<kList>(P, st, x, Tf56, 256, Tg6, Vhi, 32, fr >> 6, gl, gbase, L, sel);
     const uint32_t c2 = (x[1] >> 25) & 3u;
     const uint32_t c3r = (c2 ^ c) | (c << 2);
     const uint32_t c3l = (x[1] >> 27) & 15u;
@@ -324,8 +378,17 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem &M, const M
     if (!(op.flags & MF_TO_R)) st.pu = pset(st.pu, op.sh_dst, gl);
 }
 
+#ifdef QPD_STAMPS
+// Diagnostic build only: wave cycles per op class (lane k of each wave
+// accumulates class k; flushed once per wave).  Class = 2*type + (op syncs).
+__device__ unsigned long long qpd_stamp_acc[64];
+#endif
+
 template <int KIND>
-__global__ __launch_bounds__(64, 6) void lut_fast_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
+#ifndef QPD_WPE
+#define QPD_WPE 6
+#endif
+__global__ __launch_bounds__(64, QPD_WPE) void lut_fast_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
                                                          uint8_t *__restrict__ out) {
     constexpr bool kList = (KIND == K_SCL_LUT || KIND == K_FASTSCL_LUT);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
@@ -356,11 +419,28 @@ __global__ __launch_bounds__(64, 6) void lut_fast_kernel(FastPlan P, const int32
         st.ps = self;
         st.pu = self;
 
+#ifdef QPD_STAMPS
+        uint64_t stamp_acc = 0, stamp_cnt = 0;
+#endif
         MOp nxt = P.ops[0];
         Pre pre = fetch_pre(P, nxt, lane, vlane);
         for (int oi = 0; oi < P.nops; ++oi) {
+#ifndef QPD_NO_LAUNDER
+            // Re-derive the lane constants every op: without this the compiler
+            // hoists dozens of lane-derived addresses out of the op loop and
+            // pins them in VGPRs for the whole kernel (spills, low occupancy).
+            int lane = threadIdx.x;
+            asm volatile("" : "+v"(lane));
+            const int gl = lane & (gs - 1);
+            const int gbase = lane & ~(gs - 1);
+            const int vlane = lane < P.v ? lane : 0;
+#endif
             const MOp op = nxt;
             const Pre cur = pre;
+#ifdef QPD_STAMPS
+            __builtin_amdgcn_s_waitcnt(0);
+            const uint64_t stamp_t0 = __builtin_amdgcn_s_memtime();
+#endif
             if (oi + 1 < P.nops) {
                 nxt = P.ops[oi + 1];
                 pre = fetch_pre(P, nxt, lane, vlane);
@@ -417,7 +497,7 @@ __global__ __launch_bounds__(64, 6) void lut_fast_kernel(FastPlan P, const int32
                     if (!(fl & MF_TO_R)) st.pu = pset(st.pu, op.sh_dst, gl);
                     break;
                 }
-                default: {  // special nodes, FastSCLUT.cpp:46-107 / FastSCLLUTDecoder.cpp:82-213
+                default: if constexpr (KIND == K_FASTSC_LUT || KIND == K_FASTSCL_LUT) {  // special nodes, FastSCLUT.cpp:46-107 / FastSCLLUTDecoder.cpp:82-213
                     const int temp = op.cnt;
                     const int src = gbase + pfield(st.ps, op.sh_src);
                     const bool dl = fl & MF_DST_LDS;
@@ -578,7 +658,20 @@ __global__ __launch_bounds__(64, 6) void lut_fast_kernel(FastPlan P, const int32
                 }
             }
             if (fl & MF_SYNC) wave_sync();  // drain global writes before any cross-lane read
+#ifdef QPD_STAMPS
+            __builtin_amdgcn_s_waitcnt(0);
+            {
+                const uint64_t dt = __builtin_amdgcn_s_memtime() - stamp_t0;
+                const int cls = 2 * op.type + ((fl & MF_SYNC) ? 1 : 0);
+                if ((int)(threadIdx.x & 31) == cls) stamp_acc += dt;
+                if ((int)(threadIdx.x & 31) == cls) stamp_cnt += 1;
+            }
+#endif
         }
+#ifdef QPD_STAMPS
+        __builtin_amdgcn_s_waitcnt(0);
+        const uint64_t stamp_t2 = __builtin_amdgcn_s_memtime();
+#endif
 
         // Root partial sums -> u = x F^{(x)n} (FastSCLUT.cpp:186-198), R[0] rows.
         const bool rl = P.R0_lds;
@@ -617,6 +710,15 @@ __global__ __launch_bounds__(64, 6) void lut_fast_kernel(FastPlan P, const int32
             }
         }
         wave_sync();
+#ifdef QPD_STAMPS
+        __builtin_amdgcn_s_waitcnt(0);
+        if (threadIdx.x == 31) stamp_acc += __builtin_amdgcn_s_memtime() - stamp_t2;  // class 31: frame tail
+        if (threadIdx.x == 31) stamp_cnt += 1;
+        if (threadIdx.x < 32) {
+            atomicAdd(&qpd_stamp_acc[threadIdx.x], (unsigned long long)stamp_acc);
+            atomicAdd(&qpd_stamp_acc[32 + threadIdx.x], (unsigned long long)stamp_cnt);
+        }
+#endif
     }
 }
 

@@ -1,0 +1,48 @@
+"""Per-op-class wave cycles of the fast kernel (diagnostic build with -DQPD_STAMPS).
+usage: QPD_LIB=build_variants/libqpd_stamps.so python tools/stamps.py [kind N K L frames]"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import quantized_decoder_polar_codes_amd as Q  # noqa: E402
+from quantized_decoder_polar_codes_amd import _lib, codes as C, lut as LU  # noqa: E402
+
+kind = sys.argv[1] if len(sys.argv) > 1 else "SCL-LUT"
+N, K, L, F = (int(x) for x in sys.argv[2:6]) if len(sys.argv) > 5 else (1024, 512, 8, 262144)
+names = ["F", "G", "LEAF_L", "LEAF_R", "COMB", "R0", "R1", "REP", "SPC", "BOT3"]
+_, mb, fm, mm = C.construct_pw(N, K)
+nt = C.identify_nodes(N, mb).astype(np.int32)
+p = LU.minsum_uniform_luts(N)
+rng = np.random.default_rng(0)
+sym = torch.from_numpy(rng.integers(3, 13, size=(F, N), dtype=np.int32)).cuda()
+d = Q.from_packed(kind, p, K, fm, L=L, node_type=nt)
+lib = _lib.load()
+buf = (ctypes.c_ulonglong * 64)()
+d.decode_batch(sym)
+torch.cuda.synchronize()
+lib.qpd_debug_stamps(buf)
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+d.decode_batch(sym)
+e1.record()
+torch.cuda.synchronize()
+ms = e0.elapsed_time(e1)
+lib.qpd_debug_stamps(buf)
+acc = np.array(buf[:32], dtype=np.float64)
+cnt = np.array(buf[32:], dtype=np.float64)
+info = d.info()
+tasks = (F + info["frames_per_wave"] - 1) // info["frames_per_wave"]
+tot = acc.sum()
+print(f"{kind} N={N} L={L} frames={F} waves={info['max_waves']} wall {ms:.3f} ms ({F / ms / 1e3:.3f} Mframes/s)")
+print(f"total stamped wave-cycles per task {tot / tasks:,.0f}")
+for c in range(32):
+    if cnt[c] == 0:
+        continue
+    nm = "TAIL" if c == 31 else names[c // 2] + ("/sync" if c % 2 else "")
+    print(f"  {nm:12s} ops/task {cnt[c] / tasks:8.1f}  cyc/op {acc[c] / cnt[c]:9.0f}  cyc/task {acc[c] / tasks:11,.0f}  "
+          f"{100 * acc[c] / tot:5.1f}%")
