@@ -103,6 +103,8 @@ struct qpd_decoder {
     int64_t scratch_bytes_per_wave;
     int engine = QPD_ENGINE_GENERIC;
     int lds_bytes = 0;
+    int sets = 1;  // fast engine: frame sets per wave (lut_fast_kernel NS)
+    bool l8 = false;  // fast engine: list decoder with L = 8 (select_survivors8)
     DevPlan plan{};
     qpd::FastPlan fplan{};
     DeviceBuf f_tab, g_tab, fscratch, mops;
@@ -210,7 +212,6 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
         m.dst_row = to_r ? Ly.R[d] : Ly.U[d];
         if (to_r) m.flags |= MF_TO_R;
         if (Ly.lds(d)) m.flags |= MF_DST_LDS;
-        else m.flags |= MF_SYNC;
         m.sh_dst = 4 * d;
     };
     const int t = special_of(kind, node_type, posi);
@@ -243,7 +244,6 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
             m.cnt = N >> (d + 1);
             m.dst_row = Ly.S[d + 1];
             if (Ly.lds(d + 1)) m.flags |= MF_DST_LDS;
-            else m.flags |= MF_SYNC;
             m.sh_dst = 4 * (d + 1);
             if (side) {
                 m.u_row = Ly.U[d + 1];
@@ -263,7 +263,6 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
             m.cnt = frozen[k] == 1;
             m.dst_row = side ? Ly.R[n] : Ly.U[n];
             if (Ly.lds(n)) m.flags |= MF_DST_LDS;
-            else m.flags |= MF_SYNC;
             m.sh_dst = 4 * n;
             if (side) {
                 m.u_row = Ly.U[n];
@@ -287,6 +286,63 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
     out.push_back(m);
 }
 
+// Place the global-slab drains (MF_SYNC: vmcnt(0) + barrier BEFORE the op).
+// A path reads another path's slab rows only through pointer fields copied
+// at a fork, and every op that writes a depth's rows writes all lanes' own
+// columns and re-points them at themselves.  So a drain is needed only before
+// an op that reads global rows through a pointer when some global write
+// precedes a fork since the last drain; by then the stores have long
+// completed and the drain costs almost nothing.  Single-path kinds (SC, Fast
+// SC) never read another lane's rows.
+void place_syncs(std::vector<qpd::MOp> &ops, bool list) {
+    using namespace qpd;
+    bool dirty = false, exposed = false;
+    for (MOp &m : ops) {
+        m.flags &= ~MF_SYNC;
+        if (!list) continue;
+        const bool src_glb = !(m.flags & (MF_SRC_LDS | MF_CHAN));
+        const bool u_glb = (m.type == OP_G || m.type == OP_COMB || m.type == OP_LEAF_R) && !(m.flags & MF_U_LDS);
+        if (exposed && (src_glb || u_glb)) {
+            m.flags |= MF_SYNC;
+            exposed = dirty = false;
+        }
+        if (!(m.flags & MF_DST_LDS)) dirty = true;
+        bool forks = false;
+        switch (m.type) {
+            case OP_BOT3: forks = m.cnt != 0xff; break;
+            case OP_LEAF_L:
+            case OP_LEAF_R: forks = m.cnt == 0; break;
+            case OP_REP:
+            case OP_R1: forks = true; break;
+            default: break;
+        }
+        if (forks && dirty) exposed = true;
+    }
+}
+
+#ifndef QPD_DEFAULT_SETS
+#define QPD_DEFAULT_SETS 2
+#endif
+constexpr int kDefaultSets = QPD_DEFAULT_SETS;
+
+// Instantiations of lut_fast_kernel<KIND, NS, L8>.
+const void *fast_kernel(int kind, int sets, bool l8) {
+    using namespace qpd;
+#define QPD_FK(K, S, E) reinterpret_cast<const void *>(&lut_fast_kernel<K, S, E>)
+    switch (kind) {
+        case QPD_SC_LUT: return sets == 2 ? QPD_FK(K_SC_LUT, 2, false) : QPD_FK(K_SC_LUT, 1, false);
+        case QPD_FASTSC_LUT: return sets == 2 ? QPD_FK(K_FASTSC_LUT, 2, false) : QPD_FK(K_FASTSC_LUT, 1, false);
+        case QPD_SCL_LUT:
+            if (sets == 2) return l8 ? QPD_FK(K_SCL_LUT, 2, true) : QPD_FK(K_SCL_LUT, 2, false);
+            return l8 ? QPD_FK(K_SCL_LUT, 1, true) : QPD_FK(K_SCL_LUT, 1, false);
+        case QPD_FASTSCL_LUT:
+            if (sets == 2) return l8 ? QPD_FK(K_FASTSCL_LUT, 2, true) : QPD_FK(K_FASTSCL_LUT, 2, false);
+            return l8 ? QPD_FK(K_FASTSCL_LUT, 1, true) : QPD_FK(K_FASTSCL_LUT, 1, false);
+        default: return nullptr;
+    }
+#undef QPD_FK
+}
+
 int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     qpd::FastPlan &F = d->fplan;
     const int N = c->N, n = d->n, v = c->v;
@@ -307,10 +363,16 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
         for (int dd = D; dd <= n; ++dd) r += brows(dd);
         return r;
     };
-    int budget = 6 * 1024;  // measured best on MI355X: occupancy beats LDS residency of depths < 5
+    d->sets = kDefaultSets;
+    if (const char *e = getenv("QPD_SETS")) d->sets = std::min(2, std::max(1, atoi(e)));
+    d->l8 = (c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT) && d->L == 8;
+    const int NS = d->sets;
+    // LDS per wave = NS * (selection scratch + rows of depths >= D); the budget
+    // is measured: occupancy beats LDS residency of the shallow depths.
+    int budget = NS == 1 ? 6 * 1024 : 10 * 1024;
     if (const char *e = getenv("QPD_LDS_BUDGET")) budget = atoi(e);
     FastLayout Ly;
-    while (Ly.D <= n && 256 + lds_rows(Ly.D) * 256 > budget) ++Ly.D;
+    while (Ly.D <= n && NS * (qpd::kSelInts * 4 + lds_rows(Ly.D) * 256) > budget) ++Ly.D;
     F.lds_from = Ly.D;
     int rl = 0, rg = 0;
     for (int dd = 1; dd <= n - 1; ++dd) {
@@ -341,10 +403,11 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     }
     F.lds_rows = rl;
     F.glb_rows = std::max(rg, 1);
-    d->lds_bytes = 256 + rl * 256;
+    d->lds_bytes = NS * (qpd::kSelInts * 4 + rl * 256);
     std::vector<qpd::MOp> mops;
     fast_ops(mops, Ly, c->kind, N, n, v, c->frozen_bits,
              (c->kind == QPD_FASTSC_LUT || c->kind == QPD_FASTSCL_LUT) ? c->node_type : nullptr, 0, 0);
+    place_syncs(mops, c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT);
     F.nops = (int)mops.size();
     d->num_mops = F.nops;
     {
@@ -371,20 +434,15 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     if (rc) return rc;
     rc = upload(d->g_tab, gt.data(), gt.size());
     if (rc) return rc;
-    const int64_t per_wave = (int64_t)F.glb_rows * 64 * 4;
+    const int64_t per_wave = (int64_t)NS * F.glb_rows * 64 * 4;
     // Persistent grid: as many waves as can be resident at once.
     int mw = c->max_waves;
     if (mw <= 0) {
         int dev = 0, ncu = 256, per_cu = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        hipError_t oe = hipErrorInvalidValue;
-        switch (c->kind) {
-            case QPD_SC_LUT: oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, qpd::lut_fast_kernel<qpd::K_SC_LUT>, 64, d->lds_bytes); break;
-            case QPD_SCL_LUT: oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, qpd::lut_fast_kernel<qpd::K_SCL_LUT>, 64, d->lds_bytes); break;
-            case QPD_FASTSC_LUT: oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, qpd::lut_fast_kernel<qpd::K_FASTSC_LUT>, 64, d->lds_bytes); break;
-            default: oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, qpd::lut_fast_kernel<qpd::K_FASTSCL_LUT>, 64, d->lds_bytes); break;
-        }
+        const hipError_t oe =
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fast_kernel(d->kind, d->sets, d->l8), 64, d->lds_bytes);
         if (oe != hipSuccess || per_cu <= 0) per_cu = 16;
         mw = std::max(1, ncu) * per_cu;
     }
@@ -547,7 +605,7 @@ int qpd_get_info(const qpd_decoder *d, qpd_info *info) {
     info->L = d->L;
     info->v = d->v;
     info->num_ops = d->engine == QPD_ENGINE_FAST ? d->num_mops : (int32_t)d->ops_host.size();
-    info->frames_per_wave = d->plan.fpw;
+    info->frames_per_wave = d->engine == QPD_ENGINE_FAST ? d->plan.fpw * d->sets : d->plan.fpw;
     info->lanes_per_frame = d->plan.gs;
     info->max_waves = d->max_waves;
     info->scratch_bytes_per_wave = d->scratch_bytes_per_wave;
@@ -569,7 +627,8 @@ int qpd_decode(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_o
     const int grid = (int)std::min<int64_t>(groups, d->max_waves);
     hipStream_t st = (hipStream_t)stream;
     if (d->engine == QPD_ENGINE_FAST) {
-        const int64_t fgroups = (B + d->fplan.fpw - 1) / d->fplan.fpw;
+        const int64_t tw = (int64_t)d->fplan.fpw * d->sets;  // frames per wave task
+        const int64_t fgroups = (B + tw - 1) / tw;
         int fgrid = (int)std::min<int64_t>(fgroups, d->max_waves);
         // even out the rounds of the grid-stride loop (no partial last round)
         const int64_t rounds = (fgroups + fgrid - 1) / fgrid;
@@ -577,22 +636,11 @@ int qpd_decode(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_o
         const size_t lds = (size_t)d->lds_bytes;
         qpd::FastPlan fp = d->fplan;
         fp.in_vec = ((uintptr_t)d_symbols & 15u) == 0 && (fp.N & 3) == 0;
-        switch (d->kind) {
-            case QPD_SC_LUT:
-                hipLaunchKernelGGL(qpd::lut_fast_kernel<qpd::K_SC_LUT>, dim3(fgrid), dim3(64), lds, st, fp, d_symbols, B, d_out);
-                break;
-            case QPD_SCL_LUT:
-                hipLaunchKernelGGL(qpd::lut_fast_kernel<qpd::K_SCL_LUT>, dim3(fgrid), dim3(64), lds, st, fp, d_symbols, B, d_out);
-                break;
-            case QPD_FASTSC_LUT:
-                hipLaunchKernelGGL(qpd::lut_fast_kernel<qpd::K_FASTSC_LUT>, dim3(fgrid), dim3(64), lds, st, fp, d_symbols, B, d_out);
-                break;
-            case QPD_FASTSCL_LUT:
-                hipLaunchKernelGGL(qpd::lut_fast_kernel<qpd::K_FASTSCL_LUT>, dim3(fgrid), dim3(64), lds, st, fp, d_symbols, B, d_out);
-                break;
-            default:
-                return fail(QPD_E_INVALID, "bad kind");
-        }
+        const void *kfn = fast_kernel(d->kind, d->sets, d->l8);
+        if (!kfn) return fail(QPD_E_INVALID, "bad kind");
+        const int32_t *in_arg = d_symbols;
+        void *args[] = {&fp, &in_arg, &B, &d_out};
+        QPD_HIP(hipLaunchKernel(kfn, dim3(fgrid), dim3(64), args, lds, st));
         QPD_HIP(hipGetLastError());
         return QPD_OK;
     }

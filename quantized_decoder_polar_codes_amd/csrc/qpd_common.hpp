@@ -83,8 +83,8 @@ constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppXor3 = 0x1B, kDppHalfMirror 
 
 template <int CTRL>
 __device__ __forceinline__ uint64_t dpp64(uint64_t x) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, 0xF, 0xF, false);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, false);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, CTRL, 0xF, 0xF, true);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, true);
     return ((uint64_t)hi << 32) | lo;
 }
 
@@ -104,38 +104,24 @@ __device__ __forceinline__ uint64_t xor_lane8(uint64_t x, uint64_t hm) {  // hm 
 // The candidate-index tie break (partner j < gl) holds iff gl has the highest
 // bit of M set.
 template <int M>
-__device__ __forceinline__ void rank8_partner(uint64_t K, uint64_t F, uint64_t hk, uint64_t hf, int gl, int &rk,
-                                              int &rf) {
+__device__ __forceinline__ void rank8_partner(uint64_t K, uint64_t F, uint64_t F1, uint64_t hk, uint64_t hf, int gl,
+                                              int &rk, int &rf) {
     constexpr int hb = M >= 4 ? 2 : (M >= 2 ? 1 : 0);
-    const bool t = (gl >> hb) & 1;
+    const uint64_t t = (uint64_t)((gl >> hb) & 1);
     const uint64_t ok = xor_lane8<M>(K, hk), of = xor_lane8<M>(F, hf);
-    rk += (ok < K) | (t & (ok == K));
+    // (o < X) || (o == X && partner index below) == o < X + t  (no overflow: X <= +inf bits)
+    rk += ok < K + t;
     rk += of < K;
-    rf += ok <= F;
-    rf += (of < F) | (t & (of == F));
-    __builtin_amdgcn_sched_barrier(0);  // one partner at a time: bounds live temporaries
+    rf += ok < F1;
+    rf += of < F + t;
 }
 
+// Generic form: any L <= 8 (lane groups of G = pow2 >= L), `sel` = 64 ints.
 __device__ __forceinline__ Sel select_survivors(double kk, double kf, int gl, int gbase, int L, int *sel) {
 #ifdef QPD_EXP_NOSEL  // timing experiment only: wrong results
     if (L > 0) return Sel{gl, false};
 #endif
     int rk = 0, rf = 0;
-#ifndef QPD_NO_DPP_SEL
-    if (L == 8) {  // lane group of 8: all partners through DPP
-        const uint64_t K = __builtin_bit_cast(uint64_t, kk), F = __builtin_bit_cast(uint64_t, kf);
-        const uint64_t hk = dpp64<kDppHalfMirror>(K), hf = dpp64<kDppHalfMirror>(F);
-        rk = F < K;
-        rf = K <= F;
-        rank8_partner<1>(K, F, hk, hf, gl, rk, rf);
-        rank8_partner<2>(K, F, hk, hf, gl, rk, rf);
-        rank8_partner<3>(K, F, hk, hf, gl, rk, rf);
-        rank8_partner<4>(K, F, hk, hf, gl, rk, rf);
-        rank8_partner<5>(K, F, hk, hf, gl, rk, rf);
-        rank8_partner<6>(K, F, hk, hf, gl, rk, rf);
-        rank8_partner<7>(K, F, hk, hf, gl, rk, rf);
-    } else
-#endif
     for (int j = 0; j < L; ++j) {
         const double ok = shfld(kk, gbase + j);
         const double of = shfld(kf, gbase + j);
@@ -157,6 +143,35 @@ __device__ __forceinline__ Sel select_survivors(double kk, double kf, int gl, in
     Sel s;
     s.upper = c >= L;
     s.parent = s.upper ? c - L : c;
+    return s;
+}
+
+// L = 8 (lane groups of 8): ranks from the 7 DPP partners, branch-free
+// scatter (ranks >= 8 go to a per-lane junk slot), so several independent
+// selections can interleave in one basic block.  `sel` = 128 ints.
+__device__ __forceinline__ Sel select_survivors8(double kk, double kf, int gl, int gbase, int lane, int *sel) {
+#ifdef QPD_EXP_NOSEL
+    return Sel{gl, false};
+#endif
+    const uint64_t K = __builtin_bit_cast(uint64_t, kk), F = __builtin_bit_cast(uint64_t, kf);
+    const uint64_t hk = dpp64<kDppHalfMirror>(K), hf = dpp64<kDppHalfMirror>(F);
+    const uint64_t F1 = F + 1;
+    int rk = F < K, rf = K < F1;
+    rank8_partner<1>(K, F, F1, hk, hf, gl, rk, rf);
+    rank8_partner<2>(K, F, F1, hk, hf, gl, rk, rf);
+    rank8_partner<3>(K, F, F1, hk, hf, gl, rk, rf);
+    rank8_partner<4>(K, F, F1, hk, hf, gl, rk, rf);
+    rank8_partner<5>(K, F, F1, hk, hf, gl, rk, rf);
+    rank8_partner<6>(K, F, F1, hk, hf, gl, rk, rf);
+    rank8_partner<7>(K, F, F1, hk, hf, gl, rk, rf);
+    sel[rk < 8 ? gbase + rk : 64 + lane] = gl;
+    sel[rf < 8 ? gbase + rf : 64 + lane] = gl + 8;
+    lds_order();
+    const int c = sel[gbase + gl];
+    lds_order();
+    Sel s;
+    s.upper = c >= 8;
+    s.parent = c & 7;
     return s;
 }
 

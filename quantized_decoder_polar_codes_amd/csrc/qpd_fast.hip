@@ -37,7 +37,7 @@ enum MopFlag : int32_t {
     MF_DST_LDS = 2,   // destination rows in LDS
     MF_U_LDS = 4,     // U rows read by the op in LDS
     MF_TO_R = 8,      // finished node is a right child (or the root): write R, not U
-    MF_SYNC = 16,     // op touched the global slab: drain before the next op
+    MF_SYNC = 16,     // drain the global slab before this op (see place_syncs)
     MF_R_LDS = 32,    // R rows read by the op (COMB) in LDS
     MF_CHAN = 64,     // S[d] is the channel input (d == 0)
 };
@@ -72,18 +72,27 @@ struct FastPlan {
     int32_t *err;
 };
 
-// Row access in either space.  `in_lds` is wave-uniform.
+#ifndef QPD_SLAB_AUX
+#define QPD_SLAB_AUX 0  // cache-policy bits of the slab's buffer ops (2 = nt)
+#endif
+
+// Row access in either space.  `in_lds` is wave-uniform.  The global slab is
+// reached through a buffer descriptor (32-bit lane offsets; distinct
+// instructions, so the compiler never folds the two spaces into one flat
+// access that would wait on both counters).
 struct Mem {
     uint32_t *lds;
-    uint32_t *glb;
+    uint32_t *gp;               // slab base (R1 argsort arrays)
+    __amdgpu_buffer_rsrc_t rs;  // the same slab as a buffer resource
     __device__ __forceinline__ uint32_t ld(bool in_lds, int row, int lane) const {
-        return in_lds ? lds[row * 64 + lane] : glb[(size_t)row * 64 + lane];
+        if (in_lds) return lds[row * 64 + lane];
+        return __builtin_amdgcn_raw_buffer_load_b32(rs, (row * 64 + lane) * 4, 0, QPD_SLAB_AUX);
     }
     __device__ __forceinline__ void st(bool in_lds, int row, int lane, uint32_t v) const {
         if (in_lds)
             lds[row * 64 + lane] = v;
         else
-            glb[(size_t)row * 64 + lane] = v;
+            __builtin_amdgcn_raw_buffer_store_b32(v, rs, (row * 64 + lane) * 4, 0, QPD_SLAB_AUX);
     }
 };
 
@@ -153,56 +162,74 @@ __device__ __forceinline__ uint32_t fg_word(uint32_t T, uint32_t A, uint32_t B, 
     return out;
 }
 
-// f / g op (SCLLUTDecoder.cpp:83-89 / :157-164): child symbols at depth d+1.
-// Words are processed in chunks of up to 8 whose loads are all issued before
-// the first lookup: the shallow levels live in the global slab, and one HBM
-// round trip per chunk instead of per word is what bounds these ops.
-template <bool ISG>
-__device__ __forceinline__ void fg_op(const FastPlan &P, const Mem &M, const MOp &op, const int32_t *y, int src,
-                                      int usrc, uint32_t T, int lane) {
+// f / g op (SCLLUTDecoder.cpp:83-89 / :157-164): child symbols at depth d+1,
+// for each of the wave's NS frame sets.  Words are processed in chunks whose
+// loads are all issued before the first lookup: the shallow levels live in
+// the global slab, and one memory round trip per chunk instead of per word is
+// what bounds these ops.
+template <bool ISG, int NS>
+__device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], const MOp &op, const int32_t *const (&y)[NS],
+                                      const int (&src)[NS], const int (&usrc)[NS], uint32_t T, int lane) {
     const int ctemp = op.cnt;
     const bool dl = op.flags & MF_DST_LDS, ul = op.flags & MF_U_LDS;
     if (ctemp >= 64) {
         const int nwo = ctemp >> 3;  // multiple of 8
-        for (int w0 = 0; w0 < nwo; w0 += 8) {
-            uint32_t A[8], B[8], ub[2] = {0u, 0u};
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                A[k] = sym_word(P, M, op, y, src, w0 + k);
-                B[k] = sym_word(P, M, op, y, src, nwo + w0 + k);
-            }
-            if (ISG) {
-                ub[0] = M.ld(ul, op.u_row + (w0 >> 2), usrc);
-                ub[1] = M.ld(ul, op.u_row + (w0 >> 2) + 1, usrc);
-            }
+        for (int s = 0; s < NS; ++s) {
+            for (int w0 = 0; w0 < nwo; w0 += 8) {
+                uint32_t A[8], B[8], ub[2] = {0u, 0u};
 #pragma unroll
-            for (int k = 0; k < 8; ++k)
-                M.st(dl, op.dst_row + w0 + k, lane, fg_word<ISG>(T, A[k], B[k], ((ub[k >> 2] >> ((k & 3) << 3)) << 8)));
+                for (int k = 0; k < 8; ++k) {
+                    A[k] = sym_word(P, M[s], op, y[s], src[s], w0 + k);
+                    B[k] = sym_word(P, M[s], op, y[s], src[s], nwo + w0 + k);
+                }
+                if (ISG) {
+                    ub[0] = M[s].ld(ul, op.u_row + (w0 >> 2), usrc[s]);
+                    ub[1] = M[s].ld(ul, op.u_row + (w0 >> 2) + 1, usrc[s]);
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    M[s].st(dl, op.dst_row + w0 + k, lane,
+                            fg_word<ISG>(T, A[k], B[k], ((ub[k >> 2] >> ((k & 3) << 3)) << 8)));
+            }
         }
     } else if (ctemp >= 8) {
         const int nwo = ctemp >> 3;  // 1, 2 or 4
-        uint32_t A[4] = {0u, 0u, 0u, 0u}, B[4] = {0u, 0u, 0u, 0u};
+        uint32_t A[NS][4], B[NS][4], ub[NS];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (k < nwo) {
-                A[k] = sym_word(P, M, op, y, src, k);
-                B[k] = sym_word(P, M, op, y, src, nwo + k);
+        for (int s = 0; s < NS; ++s) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                A[s][k] = B[s][k] = 0u;
+                if (k < nwo) {
+                    A[s][k] = sym_word(P, M[s], op, y[s], src[s], k);
+                    B[s][k] = sym_word(P, M[s], op, y[s], src[s], nwo + k);
+                }
             }
+            ub[s] = ISG ? M[s].ld(ul, op.u_row, usrc[s]) : 0u;
         }
-        const uint32_t ub = ISG ? M.ld(ul, op.u_row, usrc) : 0u;
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (k < nwo) M.st(dl, op.dst_row + k, lane, fg_word<ISG>(T, A[k], B[k], (ub >> (k << 3)) << 8));
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < nwo) M[s].st(dl, op.dst_row + k, lane, fg_word<ISG>(T, A[s][k], B[s][k], (ub[s] >> (k << 3)) << 8));
     } else {  // ctemp in {2, 4}: the whole depth-d node (a then b) is one word
-        const uint32_t W = sym_word(P, M, op, y, src, 0, 2 * ctemp);
-        const uint32_t ub = ISG ? M.ld(ul, op.u_row, usrc) : 0u;
-        uint32_t out = 0;
-        for (int i = 0; i < ctemp; ++i) {
-            uint32_t idx = (((W >> (4 * i)) & 15u) << 4) | ((W >> (4 * (i + ctemp))) & 15u);
-            if (ISG) idx |= ((ub >> i) & 1u) << 8;
-            out |= lut4(T, idx) << (4 * i);
+        uint32_t W[NS], ub[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            W[s] = sym_word(P, M[s], op, y[s], src[s], 0, 2 * ctemp);
+            ub[s] = ISG ? M[s].ld(ul, op.u_row, usrc[s]) : 0u;
         }
-        M.st(dl, op.dst_row, lane, out);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            uint32_t out = 0;
+            for (int i = 0; i < ctemp; ++i) {
+                uint32_t idx = (((W[s] >> (4 * i)) & 15u) << 4) | ((W[s] >> (4 * (i + ctemp))) & 15u);
+                if (ISG) idx |= ((ub[s] >> i) & 1u) << 8;
+                out |= lut4(T, idx) << (4 * i);
+            }
+            M[s].st(dl, op.dst_row, lane, out);
+        }
     }
 }
 
@@ -234,20 +261,28 @@ __device__ __forceinline__ Pre fetch_pre(const FastPlan &P, const MOp &op, int l
 }
 
 // ---------------------------------------------------------------------------
-// List state and the fork (mink, SCLLUTDecoder.cpp:105-144)
+// List state and the fork (mink, SCLLUTDecoder.cpp:105-144).
+//
+// A wave runs NS independent frame sets through the same op stream.  The op
+// records, the per-node tables and all scalar control are shared; the sets'
+// dependency chains (LDS lookups, survivor selection, fork shuffles) are
+// independent and interleave, which hides the LDS latency that bounds a
+// single set.
 // ---------------------------------------------------------------------------
 struct Path {
     double pm;
     uint64_t ps, pu;
 };
 
+constexpr int kSelInts = 128;  // per set: 64 slots + 64 junk slots (select_survivors8)
+
 // Info leaf with quanta dm: keep the L best of {keep, flip} candidates.
 // Returns the new decision; `extra` words follow the surviving lineage.
-template <int NX>
-__device__ __forceinline__ uint32_t leaf_fork(Path &st, double dm, int gl, int gbase, int L, int *sel,
+template <bool L8, int NX>
+__device__ __forceinline__ uint32_t leaf_fork(Path &st, double dm, int gl, int gbase, int L, int lane, int *sel,
                                               uint32_t (&extra)[NX]) {
     const double kf = st.pm + fabs(dm);
-    const Sel sl = select_survivors(st.pm, kf, gl, gbase, L, sel);
+    const Sel sl = L8 ? select_survivors8(st.pm, kf, gl, gbase, lane, sel) : select_survivors(st.pm, kf, gl, gbase, L, sel);
     const int p = gbase + sl.parent;
     const uint32_t hd = dm < 0;  // H4: SCL family `< 0`
     const uint32_t dec = (uint32_t)__shfl((int)hd, p) ^ (sl.upper ? 1u : 0u);
@@ -259,48 +294,77 @@ __device__ __forceinline__ uint32_t leaf_fork(Path &st, double dm, int gl, int g
     return dec;
 }
 
-// One leaf decision.  `frozen` is wave-uniform.
-template <bool kList, int NX>
-__device__ __forceinline__ uint32_t leaf_decide(Path &st, double dm, bool frozen, int gl, int gbase, int L, int *sel,
-                                                uint32_t (&extra)[NX]) {
-    if (!kList) return frozen ? 0u : (uint32_t)(dm <= 0);  // H4: SC family `<= 0`
-    if (frozen) {
-        st.pm += fabs(dm) * (double)(dm < 0);  // :100-104
-        return 0u;
+// One leaf decision for every set.  `frozen` is wave-uniform.
+template <bool kList, bool L8, int NS, int NX>
+__device__ __forceinline__ void leaf_decide(Path (&st)[NS], const double (&dm)[NS], bool frozen, int gl, int gbase,
+                                            int L, int lane, int *sel, uint32_t (&extra)[NS][NX],
+                                            uint32_t (&dec)[NS]) {
+    if (!kList) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) dec[s] = frozen ? 0u : (uint32_t)(dm[s] <= 0);  // H4: SC family `<= 0`
+        return;
     }
-    return leaf_fork(st, dm, gl, gbase, L, sel, extra);
+    if (frozen) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            st[s].pm += fabs(dm[s]) * (double)(dm[s] < 0);  // :100-104
+            dec[s] = 0u;
+        }
+        return;
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) dec[s] = leaf_fork<L8>(st[s], dm[s], gl, gbase, L, lane, sel + kSelInts * s, extra[s]);
 }
 
 // ---------------------------------------------------------------------------
 // BOT3: the height-3 subtree under a depth n-3 node, fully in registers.
 // Node numbering inside the subtree (posi): q0 = p0; q1,q2 = 2p0+1, 2p0+2;
 // q3..q6 = 4p0+3 .. 4p0+6; leaves k0..k0+7 (k0 = 8*node).
-// In-register lineage state: W3 (8 symbols of q0) and pk = W2 (bits 0-15, 4
-// symbols of the current depth n-2 node) | W1 (bits 16-23, 2 symbols) |
-// bL (bit 24, left leaf decision) | c2 (bits 25-26, left result at depth n-1)
-// | c3 (bits 27-30, left result at depth n-2).
+// In-register lineage state per set: x[0] = W3 (8 symbols of q0) and x[1] =
+// W2 (bits 0-15, 4 symbols of the current depth n-2 node) | W1 (bits 16-23,
+// 2 symbols) | bL (bit 24, left leaf decision) | c2 (bits 25-26, left result
+// at depth n-1) | c3 (bits 27-30, left result at depth n-2).
 // ---------------------------------------------------------------------------
-template <bool kList>
-__device__ __forceinline__ uint32_t bot_pair(const FastPlan &P, Path &st, uint32_t (&x)[2], uint32_t Tf, int fo,
-                                             uint32_t Tg, double V, int vo, int fr, int gl, int gbase, int L, int *sel) {
-    // x[0] = W3, x[1] = pk
-    uint32_t a = (x[1] >> 16) & 15u, b = (x[1] >> 20) & 15u;
-    double dm = 0;
-    if (kList || !(fr & 1)) dm = shfld(V, vo + (int)lut4(Tf, ((a << 4) | b) + fo));
-    const uint32_t bl = leaf_decide<kList>(st, dm, fr & 1, gl, gbase, L, sel, x);
-    x[1] = (x[1] & ~(1u << 24)) | (bl << 24);
-    a = (x[1] >> 16) & 15u;
-    b = (x[1] >> 20) & 15u;
-    const uint32_t blin = (x[1] >> 24) & 1u;
-    if (kList || !(fr & 2)) dm = shfld(V, vo + 16 + (int)lut4(Tg, (blin << 8) | (a << 4) | b));
-    const uint32_t br = leaf_decide<kList>(st, dm, fr & 2, gl, gbase, L, sel, x);
-    const uint32_t bl2 = (x[1] >> 24) & 1u;
-    return (bl2 ^ br) | (br << 1);
+__device__ __forceinline__ uint32_t f_pair(uint32_t T, int off, uint32_t w2) {  // 2 symbols of f(W2)
+    return lut4(T, off + (((w2 & 15u) << 4) | ((w2 >> 8) & 15u))) |
+           (lut4(T, off + ((((w2 >> 4) & 15u) << 4) | ((w2 >> 12) & 15u))) << 4);
+}
+__device__ __forceinline__ uint32_t g_pair(uint32_t T, uint32_t c2, uint32_t w2) {  // 2 symbols of g(W2, c2)
+    return lut4(T, ((c2 & 1u) << 8) | ((w2 & 15u) << 4) | ((w2 >> 8) & 15u)) |
+           (lut4(T, ((c2 >> 1) << 8) | (((w2 >> 4) & 15u) << 4) | ((w2 >> 12) & 15u)) << 4);
 }
 
-template <bool kList>
-__device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem &M, const MOp &op, const int32_t *y, Path &st,
-                                        uint32_t Tf0, int gl, int gbase, int L, int *sel, int lane, int vlane) {
+template <bool kList, bool L8, int NS>
+__device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], uint32_t Tf, int fo, uint32_t Tg,
+                                         double V, int vo, int fr, int gl, int gbase, int L, int lane, int *sel,
+                                         uint32_t (&c)[NS]) {
+    double dm[NS];
+    uint32_t bl[NS], br[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const uint32_t a = (x[s][1] >> 16) & 15u, b = (x[s][1] >> 20) & 15u;
+        dm[s] = 0;
+        if (kList || !(fr & 1)) dm[s] = shfld(V, vo + (int)lut4(Tf, ((a << 4) | b) + fo));
+    }
+    leaf_decide<kList, L8>(st, dm, fr & 1, gl, gbase, L, lane, sel, x, bl);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        x[s][1] = (x[s][1] & ~(1u << 24)) | (bl[s] << 24);
+        const uint32_t a = (x[s][1] >> 16) & 15u, b = (x[s][1] >> 20) & 15u;
+        if (kList || !(fr & 2)) dm[s] = shfld(V, vo + 16 + (int)lut4(Tg, (bl[s] << 8) | (a << 4) | b));
+    }
+    leaf_decide<kList, L8>(st, dm, fr & 2, gl, gbase, L, lane, sel, x, br);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const uint32_t bl2 = (x[s][1] >> 24) & 1u;
+        c[s] = (bl2 ^ br[s]) | (br[s] << 1);
+    }
+}
+
+template <bool kList, bool L8, int NS>
+__device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], const MOp &op,
+                                        const int32_t *const (&y)[NS], Path (&st)[NS], uint32_t Tf0, int gl, int gbase,
+                                        int L, int *sel, int lane) {
     const int p0 = op.tab;
     const int fr = op.cnt;
     const uint32_t *ft = P.f_tab, *gt = P.g_tab;
@@ -320,62 +384,53 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem &M, const M
     const double *vb = P.vcl + op.vrow;
     const double Vlo = s16 < v ? vb[j16 * v + s16] : 0.0;
     const double Vhi = s16 < v ? vb[(4 + j16) * v + s16] : 0.0;
-    (void)vlane;
-    uint32_t x[2];
-    x[0] = sym_word(P, M, op, y, gbase + pfield(st.ps, op.sh_src), 0);  // W3
-    x[1] = 0;
-    // ---- q0 left: W2 = f(W3)
-    uint32_t w2 = 0;
+    uint32_t x[NS][2], c[NS];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w2 |= lut4(Tf0, (((x[0] >> (4 * i)) & 15u) << 4) | ((x[0] >> (4 * i + 16)) & 15u)) << (4 * i);
-    x[1] = w2;
-    // q1: W1 = f(W2) ; leaves 0,1 ; W1 = g(W2) ; leaves 2,3
-    uint32_t w1 = lut4(Tf12, ((w2 & 15u) << 4) | ((w2 >> 8) & 15u)) | (lut4(Tf12, (((w2 >> 4) & 15u) << 4) | ((w2 >> 12) & 15u)) << 4);
-    x[1] |= w1 << 16;
-    uint32_t c = bot_pair<kList>(P, st, x, Tf34, 0, Tg3, Vlo, 0, fr, gl, gbase, L, sel);
-    x[1] = (x[1] & ~(3u << 25)) | (c << 25);
-    w2 = x[1] & 0xffffu;
-    {
-        const uint32_t c2 = (x[1] >> 25) & 3u;
-        w1 = lut4(Tg1, ((c2 & 1u) << 8) | ((w2 & 15u) << 4) | ((w2 >> 8) & 15u)) |
-             (lut4(Tg1, ((c2 >> 1) << 8) | (((w2 >> 4) & 15u) << 4) | ((w2 >> 12) & 15u)) << 4);
-    }
-    x[1] = (x[1] & ~(0xffu << 16)) | (w1 << 16);
-    c = bot_pair<kList>(P, st, x, Tf34, 256, Tg4, Vlo, 32, fr >> 2, gl, gbase, L, sel);
-    {
-        const uint32_t c2 = (x[1] >> 25) & 3u;
-        const uint32_t c3 = (c2 ^ c) | (c << 2);  // combine at depth n-2
-        x[1] = (x[1] & ~(15u << 27)) | (c3 << 27);
-    }
-    // ---- q0 right: W2 = g(W3, c3)
-    {
-        const uint32_t c3 = (x[1] >> 27) & 15u;
-        w2 = 0;
+    for (int s = 0; s < NS; ++s) x[s][0] = sym_word(P, M[s], op, y[s], gbase + pfield(st[s].ps, op.sh_src), 0);  // W3
+    // ---- q0 left: W2 = f(W3); q1: W1 = f(W2)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        uint32_t w2 = 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            w2 |= lut4(Tg0, (((c3 >> i) & 1u) << 8) | (((x[0] >> (4 * i)) & 15u) << 4) | ((x[0] >> (4 * i + 16)) & 15u))
+            w2 |= lut4(Tf0, (((x[s][0] >> (4 * i)) & 15u) << 4) | ((x[s][0] >> (4 * i + 16)) & 15u)) << (4 * i);
+        x[s][1] = w2 | (f_pair(Tf12, 0, w2) << 16);
+    }
+    bot_pair<kList, L8>(st, x, Tf34, 0, Tg3, Vlo, 0, fr, gl, gbase, L, lane, sel, c);  // leaves 0, 1
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {  // q1: W1 = g(W2, c2)
+        x[s][1] = (x[s][1] & ~(3u << 25)) | (c[s] << 25);
+        x[s][1] = (x[s][1] & ~(0xffu << 16)) | (g_pair(Tg1, c[s], x[s][1] & 0xffffu) << 16);
+    }
+    bot_pair<kList, L8>(st, x, Tf34, 256, Tg4, Vlo, 32, fr >> 2, gl, gbase, L, lane, sel, c);  // leaves 2, 3
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const uint32_t c2 = (x[s][1] >> 25) & 3u;
+        const uint32_t c3 = (c2 ^ c[s]) | (c[s] << 2);  // combine at depth n-2
+        // ---- q0 right: W2 = g(W3, c3); q2: W1 = f(W2)
+        uint32_t w2 = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            w2 |= lut4(Tg0, (((c3 >> i) & 1u) << 8) | (((x[s][0] >> (4 * i)) & 15u) << 4) |
+                                ((x[s][0] >> (4 * i + 16)) & 15u))
                   << (4 * i);
-        x[1] = (x[1] & ~0xffffu) | w2;
+        x[s][1] = w2 | (f_pair(Tf12, 256, w2) << 16) | (c3 << 27);
     }
-    w1 = lut4(Tf12, 256 + (((w2 & 15u) << 4) | ((w2 >> 8) & 15u))) |
-         (lut4(Tf12, 256 + ((((w2 >> 4) & 15u) << 4) | ((w2 >> 12) & 15u))) << 4);
-    x[1] = (x[1] & ~(0xffu << 16)) | (w1 << 16);
-    c = bot_pair<kList>(P, st, x, Tf56, 0, Tg5, Vhi, 0, fr >> 4, gl, gbase, L, sel);
-    x[1] = (x[1] & ~(3u << 25)) | (c << 25);
-    w2 = x[1] & 0xffffu;
-    {
-        const uint32_t c2 = (x[1] >> 25) & 3u;
-        w1 = lut4(Tg2, ((c2 & 1u) << 8) | ((w2 & 15u) << 4) | ((w2 >> 8) & 15u)) |
-             (lut4(Tg2, ((c2 >> 1) << 8) | (((w2 >> 4) & 15u) << 4) | ((w2 >> 12) & 15u)) << 4);
+    bot_pair<kList, L8>(st, x, Tf56, 0, Tg5, Vhi, 0, fr >> 4, gl, gbase, L, lane, sel, c);  // leaves 4, 5
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {  // q2: W1 = g(W2, c2)
+        x[s][1] = (x[s][1] & ~(3u << 25)) | (c[s] << 25);
+        x[s][1] = (x[s][1] & ~(0xffu << 16)) | (g_pair(Tg2, c[s], x[s][1] & 0xffffu) << 16);
     }
-    x[1] = (x[1] & ~(0xffu << 16)) | (w1 << 16);
-    c = bot_pair<kList>(P, st, x, Tf56, 256, Tg6, Vhi, 32, fr >> 6, gl, gbase, L, sel);
-    const uint32_t c2 = (x[1] >> 25) & 3u;
-    const uint32_t c3r = (c2 ^ c) | (c << 2);
-    const uint32_t c3l = (x[1] >> 27) & 15u;
-    const uint32_t res = (c3l ^ c3r) | (c3r << 4);  // combine at depth n-3: 8 bits
-    M.st(op.flags & MF_DST_LDS, op.dst_row, lane, res);
-    if (!(op.flags & MF_TO_R)) st.pu = pset(st.pu, op.sh_dst, gl);
+    bot_pair<kList, L8>(st, x, Tf56, 256, Tg6, Vhi, 32, fr >> 6, gl, gbase, L, lane, sel, c);  // leaves 6, 7
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const uint32_t c2 = (x[s][1] >> 25) & 3u;
+        const uint32_t c3r = (c2 ^ c[s]) | (c[s] << 2);
+        const uint32_t c3l = (x[s][1] >> 27) & 15u;
+        M[s].st(op.flags & MF_DST_LDS, op.dst_row, lane, (c3l ^ c3r) | (c3r << 4));  // combine at depth n-3
+        if (!(op.flags & MF_TO_R)) st[s].pu = pset(st[s].pu, op.sh_dst, gl);
+    }
 }
 
 #ifdef QPD_STAMPS
@@ -384,48 +439,56 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem &M, const M
 __device__ unsigned long long qpd_stamp_acc[64];
 #endif
 
-template <int KIND>
-#ifndef QPD_WPE
-#define QPD_WPE 6
+// Waves per SIMD the register allocation targets: 6 (80 VGPRs) for one
+// frame set, 4 (128 VGPRs) for two -- the measured optima on MI355X.
+#ifndef QPD_WPE1
+#define QPD_WPE1 6
 #endif
-__global__ __launch_bounds__(64, QPD_WPE) void lut_fast_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
-                                                         uint8_t *__restrict__ out) {
+#ifndef QPD_WPE2
+#define QPD_WPE2 4
+#endif
+// NS frame sets per wave (see above); L8: list decoders with L = 8.
+// LDS: NS * kSelInts ints of selection scratch, then NS * lds_rows rows.
+// Global slab: NS * glb_rows rows per workgroup.
+template <int KIND, int NS, bool L8>
+__global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : QPD_WPE1) void lut_fast_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
+                                                               uint8_t *__restrict__ out) {
     constexpr bool kList = (KIND == K_SCL_LUT || KIND == K_FASTSCL_LUT);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
-    int *sel = (int *)lds_dyn;  // 64 ints of survivor-selection scratch
-    Mem M;
-    M.lds = lds_dyn + 64;
-    M.glb = P.scratch + (size_t)blockIdx.x * P.glb_rows * 64;
-    const int lane = threadIdx.x;
+    int *const sel_all = (int *)lds_dyn;
+    Mem Mv[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        Mv[s].lds = lds_dyn + NS * kSelInts + s * P.lds_rows * 64;
+        Mv[s].gp = P.scratch + ((size_t)blockIdx.x * NS + s) * P.glb_rows * 64;
+        Mv[s].rs = __builtin_amdgcn_make_buffer_rsrc(Mv[s].gp, 0, P.glb_rows * 256, 0x00020000);
+    }
     const int gs = P.gs;
-    const int gl = lane & (gs - 1);
-    const int gbase = lane & ~(gs - 1);
     const int L = kList ? P.L : 1;
     const int N = P.N;
-    const int vlane = lane < P.v ? lane : 0;
-    const int64_t ngroups = (B + P.fpw - 1) / P.fpw;
+    const int64_t fpw = P.fpw;  // frames per set
+    const int64_t ntasks = (B + NS * fpw - 1) / (NS * fpw);
     const double kInf = __builtin_huge_val();
 
-    uint64_t self = 0;
-    for (int d = 0; d < kMaxDepth; ++d) self |= (uint64_t)gl << (4 * d);
-
-    for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
-        int64_t frame = grp * P.fpw + lane / gs;
-        const bool frame_ok = frame < B;
-        if (!frame_ok) frame = B - 1;
-        const int32_t *y = in + frame * (int64_t)N;
-        Path st;
-        st.pm = (gl == 0) ? 0.0 : kInf;
-        st.ps = self;
-        st.pu = self;
-
+    for (int64_t task = blockIdx.x; task < ntasks; task += gridDim.x) {
+        Path stv[NS];
+        {
+            const int lane = threadIdx.x, gl = lane & (gs - 1);
+            uint64_t self = 0;
+            for (int d = 0; d < kMaxDepth; ++d) self |= (uint64_t)gl << (4 * d);
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                stv[s].pm = (gl == 0) ? 0.0 : kInf;
+                stv[s].ps = self;
+                stv[s].pu = self;
+            }
+        }
 #ifdef QPD_STAMPS
         uint64_t stamp_acc = 0, stamp_cnt = 0;
 #endif
         MOp nxt = P.ops[0];
-        Pre pre = fetch_pre(P, nxt, lane, vlane);
+        Pre pre = fetch_pre(P, nxt, threadIdx.x, threadIdx.x < P.v ? threadIdx.x : 0);
         for (int oi = 0; oi < P.nops; ++oi) {
-#ifndef QPD_NO_LAUNDER
             // Re-derive the lane constants every op: without this the compiler
             // hoists dozens of lane-derived addresses out of the op loop and
             // pins them in VGPRs for the whole kernel (spills, low occupancy).
@@ -434,7 +497,14 @@ __global__ __launch_bounds__(64, QPD_WPE) void lut_fast_kernel(FastPlan P, const
             const int gl = lane & (gs - 1);
             const int gbase = lane & ~(gs - 1);
             const int vlane = lane < P.v ? lane : 0;
-#endif
+            const int32_t *yv[NS];
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                int64_t f = (task * NS + s) * fpw + lane / gs;
+                if (f >= B) f = B - 1;
+                yv[s] = in + f * (int64_t)N;
+            }
+            if (nxt.flags & MF_SYNC) wave_sync();  // before the next prefetch is issued
             const MOp op = nxt;
             const Pre cur = pre;
 #ifdef QPD_STAMPS
@@ -448,216 +518,247 @@ __global__ __launch_bounds__(64, QPD_WPE) void lut_fast_kernel(FastPlan P, const
             const int fl = op.flags;
             switch (op.type) {
                 case OP_BOT3:
-                    bot3_op<kList>(P, M, op, y, st, cur.T, gl, gbase, L, sel, lane, vlane);
+                    bot3_op<kList, L8>(P, Mv, op, yv, stv, cur.T, gl, gbase, L, sel_all, lane);
                     break;
                 case OP_F:
-                    fg_op<false>(P, M, op, y, gbase + pfield(st.ps, op.sh_src), 0, cur.T, lane);
-                    st.ps = pset(st.ps, op.sh_dst, gl);
+                case OP_G: {
+                    int src[NS], usrc[NS];
+#pragma unroll
+                    for (int s = 0; s < NS; ++s) {
+                        src[s] = gbase + pfield(stv[s].ps, op.sh_src);
+                        usrc[s] = gbase + pfield(stv[s].pu, op.sh_u);
+                    }
+                    if (op.type == OP_F)
+                        fg_op<false>(P, Mv, op, yv, src, usrc, cur.T, lane);
+                    else
+                        fg_op<true>(P, Mv, op, yv, src, usrc, cur.T, lane);
+#pragma unroll
+                    for (int s = 0; s < NS; ++s) stv[s].ps = pset(stv[s].ps, op.sh_dst, gl);
                     break;
-                case OP_G:
-                    fg_op<true>(P, M, op, y, gbase + pfield(st.ps, op.sh_src), gbase + pfield(st.pu, op.sh_u), cur.T,
-                                lane);
-                    st.ps = pset(st.ps, op.sh_dst, gl);
-                    break;
+                }
                 case OP_LEAF_L:
                 case OP_LEAF_R: {
                     const bool right = op.type == OP_LEAF_R;
                     const bool frozen = op.cnt != 0;
-                    double dm = 0;
-                    if (kList || !frozen) {
-                        const uint32_t W = sym_word(P, M, op, y, gbase + pfield(st.ps, op.sh_src), 0, 2);
-                        uint32_t idx = ((W & 15u) << 4) | ((W >> 4) & 15u);
-                        if (right) idx |= (M.ld(fl & MF_U_LDS, op.u_row, gbase + pfield(st.pu, op.sh_u)) & 1u) << 8;
-                        dm = shfld(cur.V, (int)lut4(cur.T, idx));  // vcl[n-1][k][s] (H3)
+                    double dm[NS];
+                    uint32_t none[NS][1], dec[NS];
+#pragma unroll
+                    for (int s = 0; s < NS; ++s) {
+                        dm[s] = 0;
+                        none[s][0] = 0;
+                        if (kList || !frozen) {
+                            const uint32_t W = sym_word(P, Mv[s], op, yv[s], gbase + pfield(stv[s].ps, op.sh_src), 0, 2);
+                            uint32_t idx = ((W & 15u) << 4) | ((W >> 4) & 15u);
+                            if (right)
+                                idx |= (Mv[s].ld(fl & MF_U_LDS, op.u_row, gbase + pfield(stv[s].pu, op.sh_u)) & 1u) << 8;
+                            dm[s] = shfld(cur.V, (int)lut4(cur.T, idx));  // vcl[n-1][k][s] (H3)
+                        }
                     }
-                    uint32_t none[1] = {0};
-                    const uint32_t dec = leaf_decide<kList>(st, dm, frozen, gl, gbase, L, sel, none);
-                    M.st(fl & MF_DST_LDS, op.dst_row, lane, dec);
-                    if (!right) st.pu = pset(st.pu, op.sh_dst, gl);
+                    leaf_decide<kList, L8>(stv, dm, frozen, gl, gbase, L, lane, sel_all, none, dec);
+#pragma unroll
+                    for (int s = 0; s < NS; ++s) {
+                        Mv[s].st(fl & MF_DST_LDS, op.dst_row, lane, dec[s]);
+                        if (!right) stv[s].pu = pset(stv[s].pu, op.sh_dst, gl);
+                    }
                     break;
                 }
                 case OP_COMB: {
                     const int ctemp = op.cnt;
-                    const int usrc = gbase + pfield(st.pu, op.sh_u);
                     const bool ul = fl & MF_U_LDS, rl = fl & MF_R_LDS, dl = fl & MF_DST_LDS;
                     if (ctemp < 32) {
                         const uint32_t m = (1u << ctemp) - 1u;
-                        const uint32_t u = M.ld(ul, op.u_row, usrc) & m;
-                        const uint32_t r = M.ld(rl, op.r_row, lane) & m;
-                        M.st(dl, op.dst_row, lane, (u ^ r) | (r << ctemp));
+                        uint32_t u[NS], r[NS];
+#pragma unroll
+                        for (int s = 0; s < NS; ++s) {
+                            u[s] = Mv[s].ld(ul, op.u_row, gbase + pfield(stv[s].pu, op.sh_u)) & m;
+                            r[s] = Mv[s].ld(rl, op.r_row, lane) & m;
+                        }
+#pragma unroll
+                        for (int s = 0; s < NS; ++s) Mv[s].st(dl, op.dst_row, lane, (u[s] ^ r[s]) | (r[s] << ctemp));
                     } else {
                         const int cw = ctemp >> 5;
-                        for (int w = 0; w < cw; ++w) {
-                            const uint32_t u = M.ld(ul, op.u_row + w, usrc);
-                            const uint32_t r = M.ld(rl, op.r_row + w, lane);
-                            M.st(dl, op.dst_row + w, lane, u ^ r);
-                            M.st(dl, op.dst_row + cw + w, lane, r);
+#pragma unroll
+                        for (int s = 0; s < NS; ++s) {
+                            const int usrc = gbase + pfield(stv[s].pu, op.sh_u);
+                            for (int w = 0; w < cw; ++w) {
+                                const uint32_t u = Mv[s].ld(ul, op.u_row + w, usrc);
+                                const uint32_t r = Mv[s].ld(rl, op.r_row + w, lane);
+                                Mv[s].st(dl, op.dst_row + w, lane, u ^ r);
+                                Mv[s].st(dl, op.dst_row + cw + w, lane, r);
+                            }
                         }
                     }
-                    if (!(fl & MF_TO_R)) st.pu = pset(st.pu, op.sh_dst, gl);
+                    if (!(fl & MF_TO_R)) {
+#pragma unroll
+                        for (int s = 0; s < NS; ++s) stv[s].pu = pset(stv[s].pu, op.sh_dst, gl);
+                    }
                     break;
                 }
                 default: if constexpr (KIND == K_FASTSC_LUT || KIND == K_FASTSCL_LUT) {  // special nodes, FastSCLUT.cpp:46-107 / FastSCLLUTDecoder.cpp:82-213
-                    const int temp = op.cnt;
-                    const int src = gbase + pfield(st.ps, op.sh_src);
-                    const bool dl = fl & MF_DST_LDS;
-                    const int nwo = (temp + 31) >> 5;
-                    const double *vq = P.vcl + (size_t)op.vrow * P.v;  // row d-1, position temp*node
-                    auto sym = [&](int j) -> int {
-                        const uint32_t w = M.ld(fl & MF_SRC_LDS, op.src_row + (j >> 3), src);
-                        return (int)((w >> ((j & 7) << 2)) & 15u);
-                    };
-                    auto llr = [&](int j) -> double { return vq[(size_t)j * P.v + sym(j)]; };
-                    if (op.type == OP_R0) {
-                        if (kList) {
-                            for (int j = 0; j < temp; ++j) {
-                                const double l = llr(j);
-                                st.pm += (double)(float)(l < 0) * fabs(l);
-                            }
-                        }
-                        for (int w = 0; w < nwo; ++w) M.st(dl, op.dst_row + w, lane, 0u);
-                    } else if (op.type == OP_REP) {
-                        uint32_t fill = 0;
-                        if (!kList) {
-                            double S = 0;
-                            for (int j = 0; j < temp; ++j) S += llr(j);
-                            fill = S <= 0 ? 0xffffffffu : 0u;
-                        } else {
-                            double kk = st.pm, kf = st.pm;
-                            for (int j = 0; j < temp; ++j) {
-                                const double l = llr(j);
-                                kk += (double)(l < 0) * fabs(l);
-                                kf += (double)(l >= 0) * fabs(l);
-                            }
-                            const Sel sl = select_survivors(kk, kf, gl, gbase, L, sel);
-                            const int p = gbase + sl.parent;
-                            st.pm = pick(sl.upper, shfld(kf, p), shfld(kk, p));
-                            st.ps = shfl64(st.ps, p);
-                            st.pu = shfl64(st.pu, p);
-                            fill = sl.upper ? 0xffffffffu : 0u;
-                        }
-                        const uint32_t m = temp < 32 ? ((1u << temp) - 1u) : 0xffffffffu;
-                        for (int w = 0; w < nwo; ++w) M.st(dl, op.dst_row + w, lane, fill & m);
-                    } else if (op.type == OP_SPC) {  // FastSC only
-                        uint32_t parity = 0;
-                        double best = 0;
-                        int bi = 0;
-                        for (int w = 0; w < nwo; ++w) {
-                            uint32_t word = 0;
-                            for (int i = 0; i < 32 && 32 * w + i < temp; ++i) {
-                                const int j = 32 * w + i;
-                                const double l = llr(j);
-                                const uint32_t h = l <= 0;
-                                word |= h << i;
-                                parity ^= h;
-                                const double a = fabs(l);
-                                if (j == 0 || a < best) {  // first minimum (H6)
-                                    best = a;
-                                    bi = j;
+                  for (int s = 0; s < NS; ++s) {
+                    Path &st = stv[s];
+                    const Mem &M = Mv[s];
+                    int *const sel = sel_all + kSelInts * s;
+                        const int temp = op.cnt;
+                        const int src = gbase + pfield(st.ps, op.sh_src);
+                        const bool dl = fl & MF_DST_LDS;
+                        const int nwo = (temp + 31) >> 5;
+                        const double *vq = P.vcl + (size_t)op.vrow * P.v;  // row d-1, position temp*node
+                        auto sym = [&](int j) -> int {
+                            const uint32_t w = M.ld(fl & MF_SRC_LDS, op.src_row + (j >> 3), src);
+                            return (int)((w >> ((j & 7) << 2)) & 15u);
+                        };
+                        auto llr = [&](int j) -> double { return vq[(size_t)j * P.v + sym(j)]; };
+                        if (op.type == OP_R0) {
+                            if (kList) {
+                                for (int j = 0; j < temp; ++j) {
+                                    const double l = llr(j);
+                                    st.pm += (double)(float)(l < 0) * fabs(l);
                                 }
                             }
-                            M.st(dl, op.dst_row + w, lane, word);
-                        }
-                        if (parity) {
-                            const int row = op.dst_row + (bi >> 5);
-                            M.st(dl, row, lane, M.ld(dl, row, lane) ^ (1u << (bi & 31)));
-                        }
-                    } else if (!kList) {  // OP_R1, FastSC: `<= 0`
-                        for (int w = 0; w < nwo; ++w) {
-                            uint32_t word = 0;
-                            for (int i = 0; i < 32 && 32 * w + i < temp; ++i) word |= (uint32_t)(llr(32 * w + i) <= 0) << i;
-                            M.st(dl, op.dst_row + w, lane, word);
-                        }
-                    } else if constexpr (KIND == K_FASTSCL_LUT) {  // OP_R1, FastSCL: :99-166
-                        const int m = (L - 1) < temp ? (L - 1) : temp;
-                        uint32_t *g = M.glb;
-                        for (int w = 0; w < nwo; ++w) {
-                            uint32_t word = 0;
-                            for (int i = 0; i < 32 && 32 * w + i < temp; ++i) {
-                                const int j = 32 * w + i;
-                                const double l = llr(j);
-                                word |= (uint32_t)(l < 0) << i;
-                                ((double *)(g + (size_t)(P.K_row + 2 * j) * 64))[lane] = fabs(l);
-                            }
-                            g[(size_t)(P.H_row + w) * 64 + lane] = word;
-                        }
-                        int ord[kMaxM];
-                        double ms[kMaxM];
-                        int flip[kMaxM];
-#pragma unroll
-                        for (int q = 0; q < kMaxM; ++q) {
-                            ord[q] = 0;
-                            ms[q] = 0;
-                            flip[q] = -1;
-                        }
-                        FastSortSeq seq{g, P.I_row, P.K_row, lane};
-                        if (temp <= stl::kThreshold) {
-                            uint32_t taken = 0;
-#pragma unroll
-                            for (int q = 0; q < kMaxM; ++q) {
-                                if (q < m) {
-                                    int bj = -1;
-                                    double bk = 0;
-                                    for (int j = 0; j < temp; ++j) {
-                                        if (taken & (1u << j)) continue;
-                                        const double kj = seq.key(j);
-                                        if (bj < 0 || kj < bk) {
-                                            bj = j;
-                                            bk = kj;
-                                        }
-                                    }
-                                    taken |= 1u << bj;
-                                    ord[q] = bj;
-                                    ms[q] = bk;
+                            for (int w = 0; w < nwo; ++w) M.st(dl, op.dst_row + w, lane, 0u);
+                        } else if (op.type == OP_REP) {
+                            uint32_t fill = 0;
+                            if (!kList) {
+                                double S = 0;
+                                for (int j = 0; j < temp; ++j) S += llr(j);
+                                fill = S <= 0 ? 0xffffffffu : 0u;
+                            } else {
+                                double kk = st.pm, kf = st.pm;
+                                for (int j = 0; j < temp; ++j) {
+                                    const double l = llr(j);
+                                    kk += (double)(l < 0) * fabs(l);
+                                    kf += (double)(l >= 0) * fabs(l);
                                 }
-                            }
-                        } else {
-                            for (int p = 0; p < temp; ++p) seq.set(p, p);
-                            stl::sort(seq, 0, temp);
-#pragma unroll
-                            for (int q = 0; q < kMaxM; ++q) {
-                                if (q < m) {
-                                    ord[q] = seq.get(q);
-                                    ms[q] = seq.key(ord[q]);
-                                }
-                            }
-                        }
-                        wave_sync();  // H rows visible to the whole wave
-                        int origin = gl;
-#pragma unroll
-                        for (int layer = 0; layer < kMaxM; ++layer) {
-                            if (layer < m) {
-                                const double kf = st.pm + ms[layer];
-                                const Sel sl = select_survivors(st.pm, kf, gl, gbase, L, sel);
+                                const Sel sl = select_survivors(kk, kf, gl, gbase, L, sel);
                                 const int p = gbase + sl.parent;
-                                const int pos_old = ord[layer];  // H2
-                                st.pm = pick(sl.upper, shfld(kf, p), shfld(st.pm, p));
+                                st.pm = pick(sl.upper, shfld(kf, p), shfld(kk, p));
                                 st.ps = shfl64(st.ps, p);
                                 st.pu = shfl64(st.pu, p);
-                                origin = __shfl(origin, p);
-#pragma unroll
-                                for (int q = 0; q < kMaxM; ++q) {
-                                    ord[q] = __shfl(ord[q], p);
-                                    ms[q] = shfld(ms[q], p);
-                                    if (q < layer) flip[q] = __shfl(flip[q], p);
+                                fill = sl.upper ? 0xffffffffu : 0u;
+                            }
+                            const uint32_t m = temp < 32 ? ((1u << temp) - 1u) : 0xffffffffu;
+                            for (int w = 0; w < nwo; ++w) M.st(dl, op.dst_row + w, lane, fill & m);
+                        } else if (op.type == OP_SPC) {  // FastSC only
+                            uint32_t parity = 0;
+                            double best = 0;
+                            int bi = 0;
+                            for (int w = 0; w < nwo; ++w) {
+                                uint32_t word = 0;
+                                for (int i = 0; i < 32 && 32 * w + i < temp; ++i) {
+                                    const int j = 32 * w + i;
+                                    const double l = llr(j);
+                                    const uint32_t h = l <= 0;
+                                    word |= h << i;
+                                    parity ^= h;
+                                    const double a = fabs(l);
+                                    if (j == 0 || a < best) {  // first minimum (H6)
+                                        best = a;
+                                        bi = j;
+                                    }
                                 }
-                                flip[layer] = sl.upper ? pos_old : -1;
+                                M.st(dl, op.dst_row + w, lane, word);
+                            }
+                            if (parity) {
+                                const int row = op.dst_row + (bi >> 5);
+                                M.st(dl, row, lane, M.ld(dl, row, lane) ^ (1u << (bi & 31)));
+                            }
+                        } else if (!kList) {  // OP_R1, FastSC: `<= 0`
+                            for (int w = 0; w < nwo; ++w) {
+                                uint32_t word = 0;
+                                for (int i = 0; i < 32 && 32 * w + i < temp; ++i) word |= (uint32_t)(llr(32 * w + i) <= 0) << i;
+                                M.st(dl, op.dst_row + w, lane, word);
+                            }
+                        } else if constexpr (KIND == K_FASTSCL_LUT) {  // OP_R1, FastSCL: :99-166
+                            const int m = (L - 1) < temp ? (L - 1) : temp;
+                            uint32_t *g = M.gp;
+                            for (int w = 0; w < nwo; ++w) {
+                                uint32_t word = 0;
+                                for (int i = 0; i < 32 && 32 * w + i < temp; ++i) {
+                                    const int j = 32 * w + i;
+                                    const double l = llr(j);
+                                    word |= (uint32_t)(l < 0) << i;
+                                    ((double *)(g + (size_t)(P.K_row + 2 * j) * 64))[lane] = fabs(l);
+                                }
+                                g[(size_t)(P.H_row + w) * 64 + lane] = word;
+                            }
+                            int ord[kMaxM];
+                            double ms[kMaxM];
+                            int flip[kMaxM];
+    #pragma unroll
+                            for (int q = 0; q < kMaxM; ++q) {
+                                ord[q] = 0;
+                                ms[q] = 0;
+                                flip[q] = -1;
+                            }
+                            FastSortSeq seq{g, P.I_row, P.K_row, lane};
+                            if (temp <= stl::kThreshold) {
+                                uint32_t taken = 0;
+    #pragma unroll
+                                for (int q = 0; q < kMaxM; ++q) {
+                                    if (q < m) {
+                                        int bj = -1;
+                                        double bk = 0;
+                                        for (int j = 0; j < temp; ++j) {
+                                            if (taken & (1u << j)) continue;
+                                            const double kj = seq.key(j);
+                                            if (bj < 0 || kj < bk) {
+                                                bj = j;
+                                                bk = kj;
+                                            }
+                                        }
+                                        taken |= 1u << bj;
+                                        ord[q] = bj;
+                                        ms[q] = bk;
+                                    }
+                                }
+                            } else {
+                                for (int p = 0; p < temp; ++p) seq.set(p, p);
+                                stl::sort(seq, 0, temp);
+    #pragma unroll
+                                for (int q = 0; q < kMaxM; ++q) {
+                                    if (q < m) {
+                                        ord[q] = seq.get(q);
+                                        ms[q] = seq.key(ord[q]);
+                                    }
+                                }
+                            }
+                            wave_sync();  // H rows visible to the whole wave
+                            int origin = gl;
+    #pragma unroll
+                            for (int layer = 0; layer < kMaxM; ++layer) {
+                                if (layer < m) {
+                                    const double kf = st.pm + ms[layer];
+                                    const Sel sl = select_survivors(st.pm, kf, gl, gbase, L, sel);
+                                    const int p = gbase + sl.parent;
+                                    const int pos_old = ord[layer];  // H2
+                                    st.pm = pick(sl.upper, shfld(kf, p), shfld(st.pm, p));
+                                    st.ps = shfl64(st.ps, p);
+                                    st.pu = shfl64(st.pu, p);
+                                    origin = __shfl(origin, p);
+    #pragma unroll
+                                    for (int q = 0; q < kMaxM; ++q) {
+                                        ord[q] = __shfl(ord[q], p);
+                                        ms[q] = shfld(ms[q], p);
+                                        if (q < layer) flip[q] = __shfl(flip[q], p);
+                                    }
+                                    flip[layer] = sl.upper ? pos_old : -1;
+                                }
+                            }
+                            for (int w = 0; w < nwo; ++w) {
+                                uint32_t word = g[(size_t)(P.H_row + w) * 64 + gbase + origin];
+    #pragma unroll
+                                for (int q = 0; q < kMaxM; ++q)
+                                    if (q < m && flip[q] >= 0 && (flip[q] >> 5) == w) word ^= 1u << (flip[q] & 31);
+                                if (temp < 32) word &= (1u << temp) - 1u;
+                                M.st(dl, op.dst_row + w, lane, word);
                             }
                         }
-                        for (int w = 0; w < nwo; ++w) {
-                            uint32_t word = g[(size_t)(P.H_row + w) * 64 + gbase + origin];
-#pragma unroll
-                            for (int q = 0; q < kMaxM; ++q)
-                                if (q < m && flip[q] >= 0 && (flip[q] >> 5) == w) word ^= 1u << (flip[q] & 31);
-                            if (temp < 32) word &= (1u << temp) - 1u;
-                            M.st(dl, op.dst_row + w, lane, word);
-                        }
-                    }
                     if (!(fl & MF_TO_R)) st.pu = pset(st.pu, op.sh_dst, gl);
-                    break;
+                  }
+                  break;
                 }
             }
-            if (fl & MF_SYNC) wave_sync();  // drain global writes before any cross-lane read
 #ifdef QPD_STAMPS
             __builtin_amdgcn_s_waitcnt(0);
             {
@@ -674,39 +775,51 @@ __global__ __launch_bounds__(64, QPD_WPE) void lut_fast_kernel(FastPlan P, const
 #endif
 
         // Root partial sums -> u = x F^{(x)n} (FastSCLUT.cpp:186-198), R[0] rows.
+        const int lane = threadIdx.x;
+        const int gl = lane & (gs - 1);
+        const int gbase = lane & ~(gs - 1);
         const bool rl = P.R0_lds;
         const int r0 = P.R0_row;
         const int nwr = (N + 31) >> 5;
-        for (int w = 0; w < nwr; ++w) {
-            uint32_t x = M.ld(rl, r0 + w, lane);
-            if (N < 32) x &= (1u << N) - 1u;
-            x ^= (x >> 1) & 0x55555555u;
-            x ^= (x >> 2) & 0x33333333u;
-            x ^= (x >> 4) & 0x0f0f0f0fu;
-            x ^= (x >> 8) & 0x00ff00ffu;
-            x ^= (x >> 16) & 0x0000ffffu;
-            M.st(rl, r0 + w, lane, x);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const Mem &M = Mv[s];
+            for (int w = 0; w < nwr; ++w) {
+                uint32_t x = M.ld(rl, r0 + w, lane);
+                if (N < 32) x &= (1u << N) - 1u;
+                x ^= (x >> 1) & 0x55555555u;
+                x ^= (x >> 2) & 0x33333333u;
+                x ^= (x >> 4) & 0x0f0f0f0fu;
+                x ^= (x >> 8) & 0x00ff00ffu;
+                x ^= (x >> 16) & 0x0000ffffu;
+                M.st(rl, r0 + w, lane, x);
+            }
+            for (int mw = 1; mw < nwr; mw *= 2)
+                for (int i = 0; i < nwr; i += 2 * mw)
+                    for (int j = 0; j < mw; ++j)
+                        M.st(rl, r0 + i + j, lane, M.ld(rl, r0 + i + j, lane) ^ M.ld(rl, r0 + i + mw + j, lane));
         }
-        for (int mw = 1; mw < nwr; mw *= 2)
-            for (int i = 0; i < nwr; i += 2 * mw)
-                for (int j = 0; j < mw; ++j)
-                    M.st(rl, r0 + i + j, lane, M.ld(rl, r0 + i + j, lane) ^ M.ld(rl, r0 + i + mw + j, lane));
         wave_sync();
-        int best = 0;
-        if (kList) {
-            double bpm = shfld(st.pm, gbase);
-            for (int j = 1; j < L; ++j) {
-                const double pj = shfld(st.pm, gbase + j);
-                if (pj < bpm) {
-                    bpm = pj;
-                    best = j;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const Mem &M = Mv[s];
+            int best = 0;
+            if (kList) {
+                double bpm = shfld(stv[s].pm, gbase);
+                for (int j = 1; j < L; ++j) {
+                    const double pj = shfld(stv[s].pm, gbase + j);
+                    if (pj < bpm) {
+                        bpm = pj;
+                        best = j;
+                    }
                 }
             }
-        }
-        if (frame_ok) {
-            for (int t = gl; t < P.K; t += gs) {
-                const int pos = P.info_pos[t];
-                out[frame * P.K + t] = (uint8_t)((M.ld(rl, r0 + (pos >> 5), gbase + best) >> (pos & 31)) & 1u);
+            const int64_t frame = (task * NS + s) * fpw + lane / gs;
+            if (frame < B) {
+                for (int t = gl; t < P.K; t += gs) {
+                    const int pos = P.info_pos[t];
+                    out[frame * P.K + t] = (uint8_t)((M.ld(rl, r0 + (pos >> 5), gbase + best) >> (pos & 31)) & 1u);
+                }
             }
         }
         wave_sync();

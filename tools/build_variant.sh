@@ -9,4 +9,4 @@ mkdir -p "$ROOT/build_variants"
   -I"$ROOT/quantized_decoder_polar_codes_amd/csrc" "$@" "$ROOT/quantized_decoder_polar_codes_amd/csrc/qpd_capi.hip" \
   -o "$ROOT/build_variants/libqpd_$NAME.so" -Rpass-analysis=kernel-resource-usage 2>&1 \
   | grep -A8 "lut_fast_kernel" | grep -E "Function Name|VGPRs:|ScratchSize" \
-  | sed 's/.*remark: //; s/\[-Rpass.*//' | paste - - - | sed 's/Function Name: _ZN3qpd15lut_fast_kernel/  /'
+  | sed 's/.*remark: //; s/\[-Rpass.*//' | paste - - - | sed "s/Function Name: _ZN3qpd15lut_fast_kernel/  /"
