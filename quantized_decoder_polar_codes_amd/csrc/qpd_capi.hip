@@ -363,7 +363,7 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
         for (int dd = D; dd <= n; ++dd) r += brows(dd);
         return r;
     };
-    d->sets = kDefaultSets;
+    d->sets = c->kind == QPD_FASTSCL_LUT ? 1 : kDefaultSets;  // FastSCL's R1 argsort state spills at NS = 2
     if (const char *e = getenv("QPD_SETS")) d->sets = std::min(2, std::max(1, atoi(e)));
     d->l8 = (c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT) && d->L == 8;
     const int NS = d->sets;

@@ -72,6 +72,15 @@ struct FastPlan {
     int32_t *err;
 };
 
+// Timing experiments only (wrong results): 0 = every op reads node 0's
+// tables / the slab drops every access.
+#ifndef QPD_EXP_TABMUL
+#define QPD_EXP_TABMUL 1
+#endif
+#ifndef QPD_EXP_SLABMUL
+#define QPD_EXP_SLABMUL 1
+#endif
+
 #ifndef QPD_SLAB_AUX
 #define QPD_SLAB_AUX 0  // cache-policy bits of the slab's buffer ops (2 = nt)
 #endif
@@ -150,14 +159,38 @@ __device__ __forceinline__ uint32_t sym_word(const FastPlan &P, const Mem &M, co
     return M.ld(op.flags & MF_SRC_LDS, op.src_row + w, src);
 }
 
-template <bool ISG>
-__device__ __forceinline__ uint32_t fg_word(uint32_t T, uint32_t A, uint32_t B, uint32_t ub) {
+// NE table lookups T[a_i, b_i] (i < NE <= 8) packed as output nibbles, with
+// a_i / b_i = nibble i of A / B and table half h_i = bit i of `hi` (the g
+// table's u = 1 half, or the second of two packed f tables).  SWAR index
+// build: byte j of X / Y is the 8-bit index of element 2j / 2j+1, from which
+// one pass each derives the ds_bpermute byte address (idx >> 1, whose bits
+// 7:2 select the dword; + 128 for the upper half) and the nibble offset
+// ((idx & 7) * 4, used by v_bfe through its low 5 bits only).
+template <int NE>
+__device__ __forceinline__ uint32_t lut_vec(uint32_t T, uint32_t A, uint32_t B, uint32_t hi) {
+    const uint32_t X = ((A << 4) & 0xF0F0F0F0u) | (B & 0x0F0F0F0Fu);
+    const uint32_t Y = (A & 0xF0F0F0F0u) | ((B >> 4) & 0x0F0F0F0Fu);
+    uint32_t hx = 0, hy = 0;  // bit 2j / 2j+1 of hi -> bit 8j+7
+    if constexpr (NE == 8) {  // one multiply spreads 4 bits (no carries reach the kept bits)
+        hx = ((hi & 0x55u) * 0x02082080u) & 0x80808080u;
+        hy = (((hi >> 1) & 0x55u) * 0x02082080u) & 0x80808080u;
+    } else {
+#pragma unroll
+        for (int j = 0; 2 * j < NE; ++j) {
+            hx |= ((hi >> (2 * j)) & 1u) << (8 * j + 7);
+            hy |= ((hi >> (2 * j + 1)) & 1u) << (8 * j + 7);
+        }
+    }
+    const uint32_t XA = ((X >> 1) & 0x7F7F7F7Fu) | hx;
+    const uint32_t YA = ((Y >> 1) & 0x7F7F7F7Fu) | hy;
+    const uint32_t XS = (X << 2) & 0x1C1C1C1Cu, YS = (Y << 2) & 0x1C1C1C1Cu;
     uint32_t out = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        uint32_t idx = (((A >> (4 * i)) & 15u) << 4) | ((B >> (4 * i)) & 15u);
-        if (ISG) idx |= (ub >> i) & 256u;
-        out |= lut4(T, idx) << (4 * i);
+    for (int k = 0; k < NE; ++k) {
+        const int j = k >> 1;
+        const uint32_t WA = (k & 1) ? YA : XA, WS = (k & 1) ? YS : XS;
+        const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((WA >> (8 * j)) & 0xFFu), (int)T);
+        out |= __builtin_amdgcn_ubfe(v, WS >> (8 * j), 4) << (4 * k);
     }
     return out;
 }
@@ -189,8 +222,7 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
                 }
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
-                    M[s].st(dl, op.dst_row + w0 + k, lane,
-                            fg_word<ISG>(T, A[k], B[k], ((ub[k >> 2] >> ((k & 3) << 3)) << 8)));
+                    M[s].st(dl, op.dst_row + w0 + k, lane, lut_vec<8>(T, A[k], B[k], ub[k >> 2] >> ((k & 3) << 3)));
             }
         }
     } else if (ctemp >= 8) {
@@ -212,7 +244,7 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
         for (int s = 0; s < NS; ++s)
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (k < nwo) M[s].st(dl, op.dst_row + k, lane, fg_word<ISG>(T, A[s][k], B[s][k], (ub[s] >> (k << 3)) << 8));
+                if (k < nwo) M[s].st(dl, op.dst_row + k, lane, lut_vec<8>(T, A[s][k], B[s][k], ub[s] >> (k << 3)));
     } else {  // ctemp in {2, 4}: the whole depth-d node (a then b) is one word
         uint32_t W[NS], ub[NS];
 #pragma unroll
@@ -222,12 +254,7 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
         }
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            uint32_t out = 0;
-            for (int i = 0; i < ctemp; ++i) {
-                uint32_t idx = (((W[s] >> (4 * i)) & 15u) << 4) | ((W[s] >> (4 * (i + ctemp))) & 15u);
-                if (ISG) idx |= ((ub[s] >> i) & 1u) << 8;
-                out |= lut4(T, idx) << (4 * i);
-            }
+            const uint32_t out = ctemp == 4 ? lut_vec<4>(T, W[s], W[s] >> 16, ub[s]) : lut_vec<2>(T, W[s], W[s] >> 8, ub[s]);
             M[s].st(dl, op.dst_row, lane, out);
         }
     }
@@ -253,9 +280,9 @@ __device__ __forceinline__ Pre fetch_pre(const FastPlan &P, const MOp &op, int l
     Pre p;
     p.T = 0;
     p.V = 0;
-    if (op.type == OP_F || op.type == OP_LEAF_L) p.T = P.f_tab[op.tab + (lane & 31)];
-    if (op.type == OP_G || op.type == OP_LEAF_R) p.T = P.g_tab[op.tab + lane];
-    if (op.type == OP_BOT3) p.T = P.f_tab[op.tab * 32 + (lane & 31)];
+    if (op.type == OP_F || op.type == OP_LEAF_L) p.T = P.f_tab[op.tab * QPD_EXP_TABMUL + (lane & 31)];
+    if (op.type == OP_G || op.type == OP_LEAF_R) p.T = P.g_tab[op.tab * QPD_EXP_TABMUL + lane];
+    if (op.type == OP_BOT3) p.T = P.f_tab[op.tab * QPD_EXP_TABMUL * 32 + (lane & 31)];
     if (op.type == OP_LEAF_L || op.type == OP_LEAF_R) p.V = P.vcl[op.vrow + vlane];
     return p;
 }
@@ -325,13 +352,11 @@ __device__ __forceinline__ void leaf_decide(Path (&st)[NS], const double (&dm)[N
 // 2 symbols) | bL (bit 24, left leaf decision) | c2 (bits 25-26, left result
 // at depth n-1) | c3 (bits 27-30, left result at depth n-2).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t f_pair(uint32_t T, int off, uint32_t w2) {  // 2 symbols of f(W2)
-    return lut4(T, off + (((w2 & 15u) << 4) | ((w2 >> 8) & 15u))) |
-           (lut4(T, off + ((((w2 >> 4) & 15u) << 4) | ((w2 >> 12) & 15u))) << 4);
+__device__ __forceinline__ uint32_t f_pair(uint32_t T, uint32_t hi, uint32_t w2) {  // 2 symbols of f(W2)
+    return lut_vec<2>(T, w2, w2 >> 8, hi);
 }
 __device__ __forceinline__ uint32_t g_pair(uint32_t T, uint32_t c2, uint32_t w2) {  // 2 symbols of g(W2, c2)
-    return lut4(T, ((c2 & 1u) << 8) | ((w2 & 15u) << 4) | ((w2 >> 8) & 15u)) |
-           (lut4(T, ((c2 >> 1) << 8) | (((w2 >> 4) & 15u) << 4) | ((w2 >> 12) & 15u)) << 4);
+    return lut_vec<2>(T, w2, w2 >> 8, c2);
 }
 
 template <bool kList, bool L8, int NS>
@@ -365,7 +390,7 @@ template <bool kList, bool L8, int NS>
 __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], const MOp &op,
                                         const int32_t *const (&y)[NS], Path (&st)[NS], uint32_t Tf0, int gl, int gbase,
                                         int L, int *sel, int lane) {
-    const int p0 = op.tab;
+    const int p0 = op.tab * QPD_EXP_TABMUL;
     const int fr = op.cnt;
     const uint32_t *ft = P.f_tab, *gt = P.g_tab;
     // Tables of the 7 internal nodes (q0's f table arrives prefetched).  Two
@@ -381,7 +406,7 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
     // register: lane 16*jj + s holds leaf 4*h + jj (v <= 16).
     const int v = P.v;
     const int s16 = lane & 15, j16 = lane >> 4;
-    const double *vb = P.vcl + op.vrow;
+    const double *vb = P.vcl + op.vrow * QPD_EXP_TABMUL;
     const double Vlo = s16 < v ? vb[j16 * v + s16] : 0.0;
     const double Vhi = s16 < v ? vb[(4 + j16) * v + s16] : 0.0;
     uint32_t x[NS][2], c[NS];
@@ -390,11 +415,8 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
     // ---- q0 left: W2 = f(W3); q1: W1 = f(W2)
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-        uint32_t w2 = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            w2 |= lut4(Tf0, (((x[s][0] >> (4 * i)) & 15u) << 4) | ((x[s][0] >> (4 * i + 16)) & 15u)) << (4 * i);
-        x[s][1] = w2 | (f_pair(Tf12, 0, w2) << 16);
+        const uint32_t w2 = lut_vec<4>(Tf0, x[s][0], x[s][0] >> 16, 0u);
+        x[s][1] = w2 | (f_pair(Tf12, 0u, w2) << 16);
     }
     bot_pair<kList, L8>(st, x, Tf34, 0, Tg3, Vlo, 0, fr, gl, gbase, L, lane, sel, c);  // leaves 0, 1
 #pragma unroll
@@ -408,13 +430,8 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
         const uint32_t c2 = (x[s][1] >> 25) & 3u;
         const uint32_t c3 = (c2 ^ c[s]) | (c[s] << 2);  // combine at depth n-2
         // ---- q0 right: W2 = g(W3, c3); q2: W1 = f(W2)
-        uint32_t w2 = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            w2 |= lut4(Tg0, (((c3 >> i) & 1u) << 8) | (((x[s][0] >> (4 * i)) & 15u) << 4) |
-                                ((x[s][0] >> (4 * i + 16)) & 15u))
-                  << (4 * i);
-        x[s][1] = w2 | (f_pair(Tf12, 256, w2) << 16) | (c3 << 27);
+        const uint32_t w2 = lut_vec<4>(Tg0, x[s][0], x[s][0] >> 16, c3);
+        x[s][1] = w2 | (f_pair(Tf12, 3u, w2) << 16) | (c3 << 27);
     }
     bot_pair<kList, L8>(st, x, Tf56, 0, Tg5, Vhi, 0, fr >> 4, gl, gbase, L, lane, sel, c);  // leaves 4, 5
 #pragma unroll
@@ -461,7 +478,7 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : QPD_WPE1) void lut_fast_ke
     for (int s = 0; s < NS; ++s) {
         Mv[s].lds = lds_dyn + NS * kSelInts + s * P.lds_rows * 64;
         Mv[s].gp = P.scratch + ((size_t)blockIdx.x * NS + s) * P.glb_rows * 64;
-        Mv[s].rs = __builtin_amdgcn_make_buffer_rsrc(Mv[s].gp, 0, P.glb_rows * 256, 0x00020000);
+        Mv[s].rs = __builtin_amdgcn_make_buffer_rsrc(Mv[s].gp, 0, P.glb_rows * 256 * QPD_EXP_SLABMUL, 0x00020000);
     }
     const int gs = P.gs;
     const int L = kList ? P.L : 1;
