@@ -779,4 +779,13 @@ int qpd_debug_stamps(unsigned long long *out64) {
     return QPD_OK;
 }
 #endif
+#ifdef QPD_STAMPS_SEL
+int qpd_debug_sel_stats(unsigned long long *out64) {
+    QPD_HIP(hipDeviceSynchronize());
+    QPD_HIP(hipMemcpyFromSymbol(out64, HIP_SYMBOL(qpd::qpd_sel_stats), 64 * sizeof(unsigned long long)));
+    static const unsigned long long zero[64] = {0};
+    QPD_HIP(hipMemcpyToSymbol(HIP_SYMBOL(qpd::qpd_sel_stats), zero, sizeof(zero)));
+    return QPD_OK;
+}
+#endif
 }  // extern "C"

@@ -80,6 +80,7 @@ struct Sel {
 // lane i is lane i^m.  quad_perm gives XOR 1/2/3, row_half_mirror XOR 7, and
 // their composition XOR 4/5/6.
 constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppXor3 = 0x1B, kDppHalfMirror = 0x141;
+constexpr int kDppRowShl1 = 0x101;  // lane i <- lane i+1 within a row of 16
 
 template <int CTRL>
 __device__ __forceinline__ uint64_t dpp64(uint64_t x) {

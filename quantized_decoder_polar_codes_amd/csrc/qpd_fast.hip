@@ -301,6 +301,9 @@ struct Path {
     uint64_t ps, pu;
 };
 
+#ifdef QPD_STAMPS_SEL
+__device__ unsigned long long qpd_sel_stats[64];
+#endif
 constexpr int kSelInts = 128;  // per set: 64 slots + 64 junk slots (select_survivors8)
 
 // Info leaf with quanta dm: keep the L best of {keep, flip} candidates.
@@ -309,9 +312,53 @@ template <bool L8, int NX>
 __device__ __forceinline__ uint32_t leaf_fork(Path &st, double dm, int gl, int gbase, int L, int lane, int *sel,
                                               uint32_t (&extra)[NX]) {
     const double kf = st.pm + fabs(dm);
+#ifdef QPD_STAMPS_SEL
+    if (L8) {  // diagnostic: how often would a keep-all / identity fast path apply?
+        uint64_t K = __builtin_bit_cast(uint64_t, st.pm), F = __builtin_bit_cast(uint64_t, kf);
+        uint64_t mxk = K, mnf = F;
+        for (int m = 1; m < 8; m <<= 1) {
+            const uint64_t ok = shfl64(mxk, lane ^ m), of = shfl64(mnf, lane ^ m);
+            mxk = ok > mxk ? ok : mxk;
+            mnf = of < mnf ? of : mnf;
+        }
+        const uint64_t Kn = shfl64(K, (lane & 7) == 7 ? lane : lane + 1);
+        const bool srt = K <= Kn;
+        const bool ka = mxk <= mnf;
+        const uint64_t bka = __ballot(ka), bid = __ballot(ka && srt);
+        const uint64_t bsrt = __ballot(srt);
+        if (lane == 0) {
+            unsigned long long *c = qpd_sel_stats + 8 * (blockIdx.x & 7);
+            atomicAdd(c + 0, 1ull);
+            atomicAdd(c + 1, (unsigned long long)(bka == ~0ull));
+            atomicAdd(c + 2, (unsigned long long)(bid == ~0ull));
+            atomicAdd(c + 3, (unsigned long long)__popcll(bka) / 8);
+            atomicAdd(c + 4, (unsigned long long)__popcll(bka & bsrt));
+        }
+    }
+#endif
+    const uint32_t hd = dm < 0;  // H4: SCL family `< 0`
+#ifndef QPD_NO_FASTKEEP
+    if constexpr (L8) {
+        // Fast path, taken when it holds for every group of the wave (about
+        // 2/3 of the info leaves on the bench channel): the keeps are already
+        // in stable order (pm_0 <= ... <= pm_7) and no flip beats any keep
+        // (max pm <= every kf).  The stable sort of the 16 candidates then
+        // puts keep_j in slot j: nothing moves, the decision is the hard one.
+        const uint64_t K = __builtin_bit_cast(uint64_t, st.pm), F = __builtin_bit_cast(uint64_t, kf);
+        uint64_t mk = K;
+        uint64_t o = dpp64<kDppXor1>(mk);
+        mk = o > mk ? o : mk;
+        o = dpp64<kDppXor2>(mk);
+        mk = o > mk ? o : mk;
+        o = dpp64<kDppHalfMirror>(mk);  // lane i^7 lies in the other quad
+        mk = o > mk ? o : mk;
+        const uint64_t Kn = dpp64<kDppRowShl1>(K);  // pm of slot gl+1
+        const bool ok = F >= mk && (gl == 7 || K <= Kn);
+        if (__ballot(ok) == ~0ull) return hd;
+    }
+#endif
     const Sel sl = L8 ? select_survivors8(st.pm, kf, gl, gbase, lane, sel) : select_survivors(st.pm, kf, gl, gbase, L, sel);
     const int p = gbase + sl.parent;
-    const uint32_t hd = dm < 0;  // H4: SCL family `< 0`
     const uint32_t dec = (uint32_t)__shfl((int)hd, p) ^ (sl.upper ? 1u : 0u);
     st.pm = pick(sl.upper, shfld(kf, p), shfld(st.pm, p));
     st.ps = shfl64(st.ps, p);

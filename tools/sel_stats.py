@@ -1,0 +1,33 @@
+"""How often the info-leaf survivor selection is trivial (diagnostic build -DQPD_STAMPS_SEL).
+usage: QPD_LIB=build_variants/libqpd_selstats.so python tools/sel_stats.py [ebn0]"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+import quantized_decoder_polar_codes_amd as Q  # noqa: E402
+from quantized_decoder_polar_codes_amd import _lib, codes as C, lut as LU  # noqa: E402
+
+ebn0 = float(sys.argv[1]) if len(sys.argv) > 1 else 2.0
+N, K, L, F = 1024, 512, 8, 65536
+_, mb, fm, mm = C.construct_pw(N, K)
+p = LU.minsum_uniform_luts(N)
+d = Q.from_packed("SCL-LUT", p, K, fm, L=L)
+lib = _lib.load()
+buf = (ctypes.c_ulonglong * 64)()
+lib.qpd_debug_sel_stats(buf)
+cases = [("random 3..12", torch.from_numpy(np.random.default_rng(0).integers(3, 13, size=(F, N), dtype=np.int32)).cuda())]
+for eb in (1.0, 2.0, 3.0):
+    cases.append((f"AWGN {eb} dB", bench.synth_frames(N, K, F, eb, 1234, mb, torch.device("cuda", 0))[1]))
+for kind, sym in cases:
+    d.decode_batch(sym)
+    torch.cuda.synchronize()
+    lib.qpd_debug_sel_stats(buf)
+    a = np.array(buf[:], dtype=np.float64).reshape(8, 8).sum(axis=0)
+    print(f"{kind}: calls {a[0]:.0f}  wave keep-all {a[1] / a[0]:.3f}  wave identity {a[2] / a[0]:.3f}  "
+          f"group keep-all {a[3] / a[0] / 8:.3f}  group identity {a[4] / a[0] / 64:.3f}")

@@ -23,7 +23,10 @@ nt = C.identify_nodes(N, mb).astype(np.int32)
 p = LU.minsum_uniform_luts(N)
 rng = np.random.default_rng(0)
 maxF = max(frames_list)
-sym = torch.from_numpy(rng.integers(3, 13, size=(maxF, N), dtype=np.int32)).cuda()
+import bench  # noqa: E402
+
+# the bench's workload: reference driver channel at Eb/N0 2 dB (data-dependent paths see realistic inputs)
+sym = bench.synth_frames(N, K, maxF, float(os.environ.get("SWEEP_EBN0", "2.0")), 1234, mb, torch.device("cuda", 0))[1]
 ref = None
 for budget, F, mw in itertools.product(budgets, frames_list, waves_list):
     os.environ["QPD_LDS_BUDGET"] = str(budget)
