@@ -1,5 +1,11 @@
-from .SCDecoder import SCDecoder  # noqa: F401
-from .SCLUTDecoder import SCLUTDecoder  # noqa: F401
-from .SCLLUTDecoder import SCLLUTDecoder  # noqa: F401
-from .FastSCLUTDecoder import FastSCLUTDecoder  # noqa: F401
-from .FastSCLLUTDecoder import FastSCLLUTDecoder  # noqa: F401
+# Same shape as the reference (PolarDecoder/PolarDecoder/Decoder/__init__.py:1-3):
+# the submodules are imported, each holding its class of the same name.
+from . import (  # noqa: F401
+    CAFastSCLLUTDecoder,
+    CASCLLUTDecoder,
+    FastSCLLUTDecoder,
+    FastSCLUTDecoder,
+    SCDecoder,
+    SCLLUTDecoder,
+    SCLUTDecoder,
+)

@@ -11,11 +11,16 @@
  *                             FastSCLUT::FastSCLUT src/FastSCLUT.cpp:13-24
  *                             FastSCLLUT::FastSCLLUT src/FastSCLLUTDecoder.cpp:42-55
  *                             SC::SC              src/SCDecoder.cpp:7-12
- *                   bound at py_interface/py_{SCLUT,SCLLUT,FastSCLUT,FastSCLLUT,SC}Decoder.cpp
+ *                             CASCLLUT::CASCLLUT  src/CASCLLUTDecoder.cpp:43-62
+ *                             CAFastSCLLUT::CAFastSCLLUT src/CAFastSCLLUTDecoder.cpp:43-56
+ *                   bound at py_interface/py_{SCLUT,SCLLUT,FastSCLUT,FastSCLLUT,SC,
+ *                   CASCLLUT,CAFastSCLLUT}Decoder.cpp
  *   qpd_decode    <- SCLUT::decode   src/SCLUTDecoder.cpp:21-124
  *                    SCLLUT::decode  src/SCLLUTDecoder.cpp:47-253
  *                    FastSCLUT::decode src/FastSCLUT.cpp:27-206
  *                    FastSCLLUT::decode src/FastSCLLUTDecoder.cpp:57-408
+ *                    CASCLLUT::decode src/CASCLLUTDecoder.cpp:64-303
+ *                    CAFastSCLLUT::decode src/CAFastSCLLUTDecoder.cpp:58-454
  *                   (batched: B frames per call instead of one)
  *   qpd_decode_f64 <- SC::decode     src/SCDecoder.cpp:14-89 (float64 LLR input)
  *   qpd_decode_host / qpd_decode_f64_host: the same from host buffers
@@ -42,7 +47,7 @@
 extern "C" {
 #endif
 
-#define QPD_ABI_VERSION 1
+#define QPD_ABI_VERSION 2
 
 /* Decoder kinds (the reference's class names). */
 enum qpd_kind {
@@ -50,7 +55,9 @@ enum qpd_kind {
     QPD_SC_LUT = 1,      /* SCLUTDecoder                                      */
     QPD_SCL_LUT = 2,     /* SCLLUTDecoder                                     */
     QPD_FASTSC_LUT = 3,  /* FastSCLUTDecoder  (R0/R1/REP/SPC shortcuts)       */
-    QPD_FASTSCL_LUT = 4  /* FastSCLLUTDecoder (R0/R1/REP shortcuts; no SPC)   */
+    QPD_FASTSCL_LUT = 4, /* FastSCLLUTDecoder (R0/R1/REP shortcuts; no SPC)   */
+    QPD_CASCL_LUT = 5,   /* CASCLLUTDecoder     (SCL-LUT + CRC-aided output)   */
+    QPD_CAFASTSCL_LUT = 6 /* CAFastSCLLUTDecoder (FastSCL-LUT + CRC-aided output) */
 };
 
 enum qpd_status {
@@ -93,6 +100,17 @@ typedef struct qpd_config {
     int32_t device;             /* HIP device ordinal (-1 = current device)       */
     int32_t max_waves;          /* persistent-grid size cap (0 = default)         */
     int32_t engine;             /* enum qpd_engine (0 = auto)                     */
+    /* CRC-aided kinds only (ignored otherwise).  Output = the first A info bits
+     * of the first path, in stable path-metric order, whose info bits [0, A)
+     * reproduce bits [A, K) under the CRC (CRC::encoding, utils.cpp:77-92;
+     * coefficient j of the divisor is 1 for j in crc_loc).  The reference's CA
+     * decoders always check CRC-24 with loc {24,23,21,20,17,15,13,12,8,4,2,1,0}
+     * (CASCLLUTDecoder.h:33-34) whatever crc_n/crc_p their ctor received; the
+     * Python shim passes exactly that.  Requires 1 <= A <= K, K - A <= crc_n. */
+    int32_t A;                  /* message bits before the CRC                    */
+    int32_t crc_n;              /* CRC length, 1..32                              */
+    const int32_t *crc_loc;     /* [crc_loc_count] coefficient indices in [0, crc_n] */
+    int32_t crc_loc_count;
 } qpd_config;
 
 /* Kernel selection.  AUTO picks FAST when the tables allow it (one table per
@@ -107,7 +125,8 @@ const char *qpd_last_error(void);
 int qpd_create(const qpd_config *cfg, qpd_decoder **out);
 void qpd_destroy(qpd_decoder *dec);
 
-/* LUT kinds.  d_symbols: device int32 [B][N]; d_out: device uint8 [B][K]. */
+/* LUT kinds.  d_symbols: device int32 [B][N]; d_out: device uint8 [B][K]
+ * ([B][A] for the CRC-aided kinds; qpd_info.out_bits). */
 int qpd_decode(qpd_decoder *dec, const int32_t *d_symbols, int64_t B, uint8_t *d_out, void *stream);
 /* QPD_SC_FLOAT.  d_llr: device float64 [B][N]; d_out: device uint8 [B][K].  */
 int qpd_decode_f64(qpd_decoder *dec, const double *d_llr, int64_t B, uint8_t *d_out, void *stream);
@@ -128,7 +147,10 @@ int qpd_check_input_error(qpd_decoder *dec);
  * quantizer (<= edges[0] -> 0, >= edges[M] -> q-1, else
  * lut[bisect_left(edges[:M], llr) - 1]).  Random numbers are Philox4x32-10 of
  * (seed, global frame id), so frames do not depend on batching or sharding.
- * d_msg: device uint8 [B][K]; d_symbols: device int32 [B][N].
+ * d_msg: device uint8 [B][K]; d_symbols: device int32 [B][N].  For the
+ * CRC-aided kinds the message is A random bits followed by the first K-A bits
+ * of their CRC (the driver's CRCEnc, mainQuantizedDecoder_LLRDomain.py:153-156),
+ * and d_msg holds the A message bits ([B][A]).
  */
 typedef struct qpd_mc_channel {
     double sigma;           /* AWGN standard deviation                 */
@@ -151,6 +173,7 @@ typedef struct qpd_info {
     int32_t engine;           /* enum qpd_engine actually used               */
     int32_t lds_bytes_per_wave;
     int32_t lds_from_depth;   /* fast engine: tree depths >= this live in LDS */
+    int32_t out_bits;         /* bits per decoded frame: K, or A (CRC-aided)  */
 } qpd_info;
 int qpd_get_info(const qpd_decoder *dec, qpd_info *info);
 

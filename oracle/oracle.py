@@ -40,6 +40,9 @@ def lib():
         i32, i64 = ctypes.c_int32, ctypes.c_int64
         L.orc_decode_lut.argtypes = [i32, i32, i32, i32, i32, P, P, P, P, i32, P, P, i32, P, i32, P, i64, P]
         L.orc_decode_lut.restype = ctypes.c_int
+        L.orc_decode_lut_ca.argtypes = [i32, i32, i32, i32, i32, i32, P, P, P, P, i32, P, P, i32, P, i32, i32, P,
+                                        i32, P, i64, P]
+        L.orc_decode_lut_ca.restype = ctypes.c_int
         L.orc_decode_sc_float.argtypes = [i32, i32, P, P, i64, P]
         L.orc_decode_sc_float.restype = ctypes.c_int
         _lib = L
@@ -67,6 +70,47 @@ def decode_lut(kind: str, packed, K: int, L: int, frozen, symbols, node_type=Non
     if rc != 0:
         raise RuntimeError(f"oracle decode failed rc={rc}")
     return out
+
+
+# The CRC the reference CA decoders check (CASCLLUTDecoder.h:33-34,
+# CAFastSCLLUTDecoder.h:29-30): CRC-24, whatever crc_n/crc_p the constructor got.
+CRC24_LOC = (24, 23, 21, 20, 17, 15, 13, 12, 8, 4, 2, 1, 0)
+
+
+def decode_lut_ca(kind: str, packed, K: int, A: int, L: int, frozen, symbols, node_type=None, crc_n: int = 24,
+                  crc_loc=CRC24_LOC) -> np.ndarray:
+    """CA-SCL-LUT / CA-FastSCL-LUT (kind "CA-SCL-LUT" / "CA-FastSCL-LUT"): uint8 [B, A]."""
+    N = packed.N
+    sym = np.ascontiguousarray(np.asarray(symbols, dtype=np.int32).reshape(-1, N))
+    B = sym.shape[0]
+    out = np.zeros((B, A), dtype=np.uint8)
+    frozen = np.ascontiguousarray(np.asarray(frozen, dtype=np.int32))
+    nt = None if node_type is None else np.ascontiguousarray(np.asarray(node_type).astype(np.int32))
+    loc = np.ascontiguousarray(np.asarray(crc_loc, dtype=np.int32))
+    base = {"CA-SCL-LUT": 2, "CA-FastSCL-LUT": 4}[kind]
+    keep = (packed.lut_f, packed.f_base, packed.lut_g, packed.g_base, packed.vcl, loc)
+    rc = lib().orc_decode_lut_ca(base, N, K, A, L, packed.v, _ptr(frozen), _ptr(nt),
+                                 _ptr(packed.lut_f), _ptr(packed.f_base), packed.f_step,
+                                 _ptr(packed.lut_g), _ptr(packed.g_base), packed.g_step,
+                                 _ptr(packed.vcl), packed.vcl_rows, crc_n, _ptr(loc), len(loc), _ptr(sym), B, _ptr(out))
+    del keep
+    if rc != 0:
+        raise RuntimeError(f"oracle decode failed rc={rc}")
+    return out
+
+
+def crc_encode(info, crc_n: int = 24, crc_loc=CRC24_LOC) -> np.ndarray:
+    """CRC::encoding (utils.cpp:77-92) on rows of `info` (uint8 [B, A]) -> check bits [B, crc_n]."""
+    info = np.atleast_2d(np.asarray(info, dtype=np.uint8))
+    p = np.zeros(crc_n + 1, dtype=np.uint8)
+    p[list(crc_loc)] = 1
+    B, A = info.shape
+    u = np.zeros((B, A + crc_n), dtype=np.uint8)
+    u[:, :A] = info
+    for i in range(A):
+        rows = u[:, i] == 1
+        u[rows, i:i + crc_n + 1] ^= p
+    return u[:, A:]
 
 
 def decode_sc_float(N: int, K: int, frozen, llr) -> np.ndarray:

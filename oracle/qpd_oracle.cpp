@@ -12,6 +12,9 @@
 //   SCL-LUT         .../src/SCLLUTDecoder.cpp:47-253   (mink :8-21, argmin :25-29)
 //   FastSC-LUT      .../src/FastSCLUT.cpp:27-206
 //   FastSCL-LUT     .../src/FastSCLLUTDecoder.cpp:57-408 (argsort :7-17)
+//   CA-SCL-LUT      .../src/CASCLLUTDecoder.cpp:47-303   (CRC epilogue :263-302)
+//   CA-FastSCL-LUT  .../src/CAFastSCLLUTDecoder.cpp:57-454 (CRC epilogue :332-453)
+//   CRC::encoding   .../src/utils.cpp:77-92
 //   partial sums    .../src/utils.cpp:62-67 (u), min-sum f/g utils.cpp:26-36
 //
 // It keeps the reference's per-fork deep copies of the whole list state, so
@@ -100,6 +103,28 @@ std::vector<int> sort_index(const std::vector<double> &key) {
     std::sort(idx.begin(), idx.end(), [&key](int p, int q) { return key[p] < key[q]; });
     return idx;
 }
+
+// CRC::encoding, utils.cpp:77-92: long division of info || 0^crc_n by the
+// coefficient vector p (p[loc] = 1, utils.cpp:69-75); returns the crc_n bits
+// that follow the info bits after the division.
+std::vector<uint8_t> crc_encoding(const std::vector<uint8_t> &info, int crc_n, const std::vector<int> &p) {
+    const int A = (int)info.size();
+    std::vector<uint8_t> u(A + crc_n, 0);
+    std::memcpy(u.data(), info.data(), A);
+    for (int i = 0; i < A; ++i)
+        if (u[i] == 1)
+            for (int j = 0; j <= crc_n; ++j) u[j + i] = (uint8_t)((u[j + i] + p[j]) % 2);
+    return std::vector<uint8_t>(u.begin() + A, u.end());
+}
+
+// CRC-aided list output (CASCLLUTDecoder.cpp:263-302): walk the paths in
+// argsort(PML) order (L <= 8: libstdc++ insertion sort, stable, H1); the
+// first whose decoded info bits [0, A) reproduce bits [A, K) under the CRC
+// wins, else the first in that order.
+struct CaSpec {
+    int A = 0, crc_n = 0;
+    std::vector<int> p;  // crc_n + 1 coefficients
+};
 
 int first_argmin(const std::vector<double> &x) {
     return (int)std::distance(x.begin(), std::min_element(x.begin(), x.end()));
@@ -251,6 +276,8 @@ struct LutSCL {
     std::vector<std::vector<int>> sym;
     std::vector<std::vector<uint8_t>> ucap;
     std::vector<double> pm;
+
+    CaSpec ca;  // ca.A > 0: CRC-aided output of A bits
 
     LutSCL(const Code &c_, bool fast_) : c(c_), fast(fast_), L(c_.L) {}
 
@@ -439,6 +466,38 @@ struct LutSCL {
         for (int i = 0; i < L; ++i)
             for (int k = 0; k < N; ++k) sym[i][k] = y[k];
         visit(0, 0);
+        if (ca.A > 0) {
+            // decoded info bits of a path: ucap[n] (SCL, :268-275) or the re-encoded
+            // root partial sums (FastSCL, :338-355)
+            auto info_of = [&](int path) {
+                std::vector<uint8_t> x(ucap[path].begin() + (fast ? 0 : n * N), ucap[path].begin() + (fast ? N : (n + 1) * N));
+                if (fast) reencode(x, N);
+                std::vector<uint8_t> info;
+                for (int k = 0; k < N; ++k)
+                    if (c.frozen[k] == 0) info.push_back(x[k]);
+                return info;
+            };
+            std::vector<int> order = sort_index(pm);
+            int winner = order[0];
+            for (int i = 0; i < L; ++i) {
+                std::vector<uint8_t> info = info_of(order[i]);
+                std::vector<uint8_t> head(info.begin(), info.begin() + ca.A);
+                std::vector<uint8_t> chk = crc_encoding(head, ca.crc_n, ca.p);
+                bool pass = true;
+                for (int j = 0; j < c.K - ca.A; ++j)
+                    if (chk[j] != info[ca.A + j]) {
+                        pass = false;
+                        break;
+                    }
+                if (pass) {
+                    winner = order[i];
+                    break;
+                }
+            }
+            std::vector<uint8_t> info = info_of(winner);
+            std::memcpy(out, info.data(), ca.A);
+            return 0;
+        }
         int best = first_argmin(pm);  // H6
         if (!fast) {
             emit_info(c, &ucap[best][n * N], out);  // :244-252
@@ -503,6 +562,30 @@ int orc_decode_lut(int32_t kind, int32_t N, int32_t K, int32_t L, int32_t v, con
         return 0;
     }
     return -3;
+}
+
+// CRC-aided list decoders: kind 2 = CA-SCL-LUT, 4 = CA-FastSCL-LUT (the
+// list kinds above plus the CRC epilogue).  crc_loc lists the nonzero
+// coefficient indices (CRC::CRC, utils.cpp:69-75).  Output uint8 [B][A].
+int orc_decode_lut_ca(int32_t kind, int32_t N, int32_t K, int32_t A, int32_t L, int32_t v, const int32_t *frozen,
+                      const int32_t *node_type, const uint8_t *lut_f, const int32_t *f_base, int32_t f_step,
+                      const uint8_t *lut_g, const int32_t *g_base, int32_t g_step, const double *vcl,
+                      int32_t vcl_rows, int32_t crc_n, const int32_t *crc_loc, int32_t n_loc, const int32_t *sym,
+                      int64_t B, uint8_t *out) {
+    if (kind != 2 && kind != 4) return -3;
+    if (A < 1 || A > K || K - A > crc_n) return -1;
+    Code c = make_code(N, K, L, v, frozen, node_type, lut_f, f_base, f_step, lut_g, g_base, g_step, vcl, vcl_rows);
+    if (N < 2 || (1 << c.n) != N) return -1;
+    LutSCL dec(c, kind == 4);
+    dec.ca.A = A;
+    dec.ca.crc_n = crc_n;
+    dec.ca.p.assign(crc_n + 1, 0);
+    for (int i = 0; i < n_loc; ++i) dec.ca.p[crc_loc[i]] = 1;
+    for (int64_t b = 0; b < B; ++b) {
+        int rc = dec.run(sym + b * N, out + b * A);
+        if (rc) return rc;
+    }
+    return 0;
 }
 
 // Float SC (min-sum), SCDecoder.cpp:14-89.  llr is float64 [B][N].

@@ -12,7 +12,8 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QPD_LIB") or os.path.join(HERE, "libqpd.so")
 
-QPD_SC_FLOAT, QPD_SC_LUT, QPD_SCL_LUT, QPD_FASTSC_LUT, QPD_FASTSCL_LUT = range(5)
+QPD_SC_FLOAT, QPD_SC_LUT, QPD_SCL_LUT, QPD_FASTSC_LUT, QPD_FASTSCL_LUT, QPD_CASCL_LUT, QPD_CAFASTSCL_LUT = range(7)
+ABI_VERSION = 2
 QPD_ENGINE_AUTO, QPD_ENGINE_GENERIC, QPD_ENGINE_FAST = range(3)
 QPD_OK, QPD_E_INVALID, QPD_E_UNSUPPORTED, QPD_E_DEVICE, QPD_E_INPUT = 0, -1, -2, -3, -4
 
@@ -58,6 +59,10 @@ class QpdConfig(ctypes.Structure):
         ("device", _i32),
         ("max_waves", _i32),
         ("engine", _i32),
+        ("A", _i32),
+        ("crc_n", _i32),
+        ("crc_loc", _P),
+        ("crc_loc_count", _i32),
     ]
 
 
@@ -86,6 +91,7 @@ class QpdInfo(ctypes.Structure):
         ("engine", _i32),
         ("lds_bytes_per_wave", _i32),
         ("lds_from_depth", _i32),
+        ("out_bits", _i32),
     ]
 
 
@@ -136,7 +142,7 @@ def load():
     L.qpd_get_info.restype = ctypes.c_int
     L.qpd_mc_frames.argtypes = [_P, ctypes.POINTER(QpdMcChannel), ctypes.c_uint64, _i64, _i64, _P, _P, _P]
     L.qpd_mc_frames.restype = ctypes.c_int
-    if L.qpd_abi_version() != 1:
+    if L.qpd_abi_version() != ABI_VERSION:
         raise ImportError("libqpd.so ABI version mismatch")
     _lib = L
     return L

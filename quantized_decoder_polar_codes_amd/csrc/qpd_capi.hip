@@ -103,6 +103,11 @@ struct qpd_decoder {
     int64_t scratch_bytes_per_wave;
     int engine = QPD_ENGINE_GENERIC;
     int lds_bytes = 0;
+    int pub_kind = 0;  // the kind the caller asked for (CRC-aided kinds map to their list kind)
+    int out_bits = 0;  // bits per decoded frame: K, or A for the CRC-aided kinds
+    int ca_A = 0, crc_n = 0;
+    uint32_t crc_q = 0;
+    DeviceBuf info_mask;
     int sets = 1;  // fast engine: frame sets per wave (lut_fast_kernel NS)
     bool l8 = false;  // fast engine: list decoder with L = 8 (select_survivors8)
     DevPlan plan{};
@@ -133,7 +138,20 @@ int set_device(const qpd_decoder *d) {
 
 int validate(const qpd_config *c, int *n_out) {
     if (!c) return fail(QPD_E_INVALID, "null config");
-    if (c->kind < QPD_SC_FLOAT || c->kind > QPD_FASTSCL_LUT) return fail(QPD_E_INVALID, "unknown decoder kind");
+    if (c->kind < QPD_SC_FLOAT || c->kind > QPD_CAFASTSCL_LUT) return fail(QPD_E_INVALID, "unknown decoder kind");
+    if (c->kind == QPD_CASCL_LUT || c->kind == QPD_CAFASTSCL_LUT) {
+        // CRC-aided output (CASCLLUTDecoder.cpp:263-302): K - A > crc_n would read
+        // past the reference's check code (UB there), so it is rejected here.
+        if (c->crc_n < 1 || c->crc_n > 32) return fail(QPD_E_INVALID, "crc_n must be in [1, 32]");
+        if (c->A < 1 || c->A > c->K || c->K - c->A > c->crc_n)
+            return fail(QPD_E_INVALID, "CRC-aided kinds need 1 <= A <= K and K - A <= crc_n");
+        if (c->crc_loc_count < 0 || (c->crc_loc_count > 0 && !c->crc_loc)) return fail(QPD_E_INVALID, "bad crc_loc");
+        for (int i = 0; i < c->crc_loc_count; ++i)
+            if (c->crc_loc[i] < 0 || c->crc_loc[i] > c->crc_n) return fail(QPD_E_INVALID, "crc_loc entry outside [0, crc_n]");
+        qpd_config base = *c;
+        base.kind = c->kind == QPD_CASCL_LUT ? QPD_SCL_LUT : QPD_FASTSCL_LUT;
+        return validate(&base, n_out);
+    }
     const int n = ilog2_exact(c->N);
     if (c->N < 2 || n < 0 || n > qpd::kMaxDepth) return fail(QPD_E_INVALID, "N must be a power of two in [2, 65536]");
     if (!c->frozen_bits) return fail(QPD_E_INVALID, "frozen_bits is NULL");
@@ -468,15 +486,30 @@ int qpd_abi_version(void) { return QPD_ABI_VERSION; }
 
 const char *qpd_last_error(void) { return g_err.c_str(); }
 
-int qpd_create(const qpd_config *c, qpd_decoder **out) {
+int qpd_create(const qpd_config *cfg, qpd_decoder **out) {
     if (!out) return fail(QPD_E_INVALID, "null output handle");
     *out = nullptr;
     int n = 0;
-    int rc = validate(c, &n);
+    int rc = validate(cfg, &n);
     if (rc) return rc;
+    // The CRC-aided kinds are their list kind plus an output epilogue.
+    qpd_config cc = *cfg;
+    const bool ca = cfg->kind == QPD_CASCL_LUT || cfg->kind == QPD_CAFASTSCL_LUT;
+    if (ca) cc.kind = cfg->kind == QPD_CASCL_LUT ? QPD_SCL_LUT : QPD_FASTSCL_LUT;
+    const qpd_config *c = &cc;
     if (c->device >= 0) QPD_HIP(hipSetDevice(c->device));
 
     qpd_decoder *d = new qpd_decoder();
+    d->pub_kind = cfg->kind;
+    d->out_bits = ca ? cfg->A : cfg->K;
+    if (ca) {
+        d->ca_A = cfg->A;
+        d->crc_n = cfg->crc_n;
+        for (int i = 0; i < cfg->crc_loc_count; ++i) {
+            const int j = cfg->crc_loc[i];  // coefficient j -> register bit crc_n - j (j = 0: leading, drops out)
+            if (j >= 1) d->crc_q |= 1u << (cfg->crc_n - j);
+        }
+    }
     d->kind = c->kind;
     d->N = c->N;
     d->n = n;
@@ -558,6 +591,11 @@ int qpd_create(const qpd_config *c, qpd_decoder **out) {
     } while (0)
     QPD_TRY(upload(d->ops, s.ops.data(), s.ops.size()));
     QPD_TRY(upload(d->info_pos, info.data(), info.size()));
+    {
+        std::vector<uint32_t> mask((N + 31) / 32, 0u);
+        for (int i : info) mask[i >> 5] |= 1u << (i & 31);
+        QPD_TRY(upload(d->info_mask, mask.data(), mask.size()));
+    }
     if (c->kind != QPD_SC_FLOAT) {
         const size_t vv = (size_t)c->v * c->v;
         QPD_TRY(upload(d->lut_f, c->lut_f, (size_t)c->lut_f_count * vv));
@@ -591,6 +629,16 @@ int qpd_create(const qpd_config *c, qpd_decoder **out) {
     P.info_pos = (const int32_t *)d->info_pos.p;
     P.scratch = (uint32_t *)d->scratch.p;
     P.err = (int32_t *)d->err.p;
+    P.out_k = d->out_bits;
+    P.ca_A = d->ca_A;
+    P.crc_n = d->crc_n;
+    P.crc_q = d->crc_q;
+    P.info_mask = (const uint32_t *)d->info_mask.p;
+    d->fplan.out_k = d->out_bits;
+    d->fplan.ca_A = d->ca_A;
+    d->fplan.crc_n = d->crc_n;
+    d->fplan.crc_q = d->crc_q;
+    d->fplan.info_mask = (const uint32_t *)d->info_mask.p;
     *out = d;
     return QPD_OK;
 }
@@ -599,7 +647,8 @@ void qpd_destroy(qpd_decoder *d) { delete d; }
 
 int qpd_get_info(const qpd_decoder *d, qpd_info *info) {
     if (!d || !info) return fail(QPD_E_INVALID, "null argument");
-    info->kind = d->kind;
+    info->kind = d->pub_kind;
+    info->out_bits = d->out_bits;
     info->N = d->N;
     info->K = d->K;
     info->L = d->L;
@@ -709,7 +758,7 @@ int qpd_decode_host(qpd_decoder *d, const int32_t *h_symbols, int64_t B, uint8_t
     if (B <= 0) return B == 0 ? QPD_OK : fail(QPD_E_INVALID, "negative batch");
     int rc = set_device(d);
     if (rc) return rc;
-    const size_t in_b = (size_t)B * d->N * sizeof(int32_t), out_b = (size_t)B * d->K;
+    const size_t in_b = (size_t)B * d->N * sizeof(int32_t), out_b = (size_t)B * d->out_bits;
     if ((rc = ensure(d->h_in, d->h_in_bytes, in_b))) return rc;
     if ((rc = ensure(d->h_out, d->h_out_bytes, std::max<size_t>(1, out_b)))) return rc;
     QPD_HIP(hipMemcpy(d->h_in.p, h_symbols, in_b, hipMemcpyHostToDevice));
@@ -723,7 +772,7 @@ int qpd_decode_f64_host(qpd_decoder *d, const double *h_llr, int64_t B, uint8_t 
     if (B <= 0) return B == 0 ? QPD_OK : fail(QPD_E_INVALID, "negative batch");
     int rc = set_device(d);
     if (rc) return rc;
-    const size_t in_b = (size_t)B * d->N * sizeof(double), out_b = (size_t)B * d->K;
+    const size_t in_b = (size_t)B * d->N * sizeof(double), out_b = (size_t)B * d->out_bits;
     if ((rc = ensure(d->h_in, d->h_in_bytes, in_b))) return rc;
     if ((rc = ensure(d->h_out, d->h_out_bytes, std::max<size_t>(1, out_b)))) return rc;
     QPD_HIP(hipMemcpy(d->h_in.p, h_llr, in_b, hipMemcpyHostToDevice));
@@ -752,6 +801,9 @@ int qpd_mc_frames(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64
     std::memset(&C, 0, sizeof(C));
     C.N = d->N;
     C.K = d->K;
+    C.A = d->crc_n > 0 ? d->ca_A : d->K;
+    C.crc_n = d->crc_n;
+    C.crc_q = d->crc_q;
     C.q = ch->q;
     C.n_edges = ch->n_edges;
     C.seed_lo = (uint32_t)seed;

@@ -176,4 +176,56 @@ __device__ __forceinline__ Sel select_survivors8(double kk, double kf, int gl, i
     return s;
 }
 
+// CRC-aided choice of the output path (CASCLLUTDecoder.cpp:263-290,
+// CAFastSCLLUTDecoder.cpp:333-371): the paths in stable path-metric order
+// (argsort of L <= 8 doubles is libstdc++'s insertion sort, H1); the first
+// whose info bits [0, A) reproduce bits [A, K) under CRC::encoding
+// (utils.cpp:77-92), else the first in that order.  The reference's bit-array
+// long division is run as the equivalent MSB-first register: the divisor's
+// leading coefficient only clears the current bit, `crc_q` holds
+// coefficients 1..crc_n.  `word(w)` = this lane's decoded bits 32w..32w+31;
+// `info_mask` = wave-uniform information-position mask words.
+template <class WordFn>
+__device__ __forceinline__ int ca_winner(double pm, int gl, int gbase, int L, int N, const uint32_t *info_mask, int A,
+                                         int K, int crc_n, uint32_t crc_q, WordFn word) {
+    int rank = 0;
+    for (int j = 0; j < L; ++j) {
+        const double o = shfld(pm, gbase + j);
+        rank += (o < pm) || (o == pm && j < gl);
+    }
+    const uint32_t top = 1u << (crc_n - 1);
+    const uint32_t mask = (top << 1) - 1u;  // crc_n = 32: 0 - 1 = all ones
+    uint32_t r = 0;
+    bool pass = true;
+    int t = 0;
+    const int nw = (N + 31) >> 5;
+    for (int w = 0; w < nw && t < K; ++w) {
+        uint32_t m = info_mask[w];
+        if (!m) continue;
+        const uint32_t x = word(w);
+        while (m) {
+            const int b = __builtin_ctz(m);
+            m &= m - 1u;
+            const uint32_t bit = (x >> b) & 1u;
+            if (t < A) {
+                const uint32_t fb = bit ^ ((r & top) ? 1u : 0u);
+                r = ((r << 1) & mask) ^ (crc_q & (0u - fb));
+            } else if (t < K) {
+                pass = pass && bit == ((r >> (crc_n - 1 - (t - A))) & 1u);
+            }
+            ++t;
+        }
+    }
+    const int key = gl < L ? (pass ? rank : 8 + rank) : 64;
+    int best = 0, bk = 1 << 30;
+    for (int j = 0; j < L; ++j) {
+        const int kj = __shfl(key, gbase + j);
+        if (kj < bk) {
+            bk = kj;
+            best = j;
+        }
+    }
+    return best;
+}
+
 }  // namespace qpd

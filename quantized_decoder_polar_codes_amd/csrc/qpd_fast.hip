@@ -60,6 +60,10 @@ struct MOp {
 struct FastPlan {
     int32_t N, n, K, L, v, gs, fpw, nops, max_r1;
     int32_t in_vec;               // per launch: input rows are 16-byte aligned
+    int32_t out_k;                // output bits per frame: K, or A (CRC-aided kinds)
+    int32_t ca_A, crc_n;          // crc_n > 0: CRC-aided output (ca_winner)
+    uint32_t crc_q;
+    const uint32_t *info_mask;    // [N/32] information-position mask
     int32_t lds_rows, glb_rows, lds_from;
     int32_t R0_row, R0_lds;      // root partial sums (R[0])
     int32_t H_row, K_row, I_row;  // R1 scratch (global)
@@ -868,7 +872,10 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : QPD_WPE1) void lut_fast_ke
         for (int s = 0; s < NS; ++s) {
             const Mem &M = Mv[s];
             int best = 0;
-            if (kList) {
+            if (kList && P.crc_n > 0) {
+                best = ca_winner(stv[s].pm, gl, gbase, L, N, P.info_mask, P.ca_A, P.K, P.crc_n, P.crc_q,
+                                 [&](int w) { return M.ld(rl, r0 + w, lane); });
+            } else if (kList) {
                 double bpm = shfld(stv[s].pm, gbase);
                 for (int j = 1; j < L; ++j) {
                     const double pj = shfld(stv[s].pm, gbase + j);
@@ -880,9 +887,9 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : QPD_WPE1) void lut_fast_ke
             }
             const int64_t frame = (task * NS + s) * fpw + lane / gs;
             if (frame < B) {
-                for (int t = gl; t < P.K; t += gs) {
+                for (int t = gl; t < P.out_k; t += gs) {
                     const int pos = P.info_pos[t];
-                    out[frame * P.K + t] = (uint8_t)((M.ld(rl, r0 + (pos >> 5), gbase + best) >> (pos & 31)) & 1u);
+                    out[frame * P.out_k + t] = (uint8_t)((M.ld(rl, r0 + (pos >> 5), gbase + best) >> (pos & 31)) & 1u);
                 }
             }
         }

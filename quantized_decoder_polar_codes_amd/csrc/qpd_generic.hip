@@ -31,6 +31,10 @@ struct DevPlan {
     int32_t N, n, K, L, v, gs, fpw, nops;
     int32_t f_step, g_step, max_r1;
     int32_t rows_per_wave;
+    int32_t out_k;         // output bits per frame: K, or A (CRC-aided kinds)
+    int32_t ca_A, crc_n;   // crc_n > 0: CRC-aided output (ca_winner)
+    uint32_t crc_q;
+    const uint32_t *info_mask;  // [N/32] information-position mask
     // scratch row offsets: S[d] (symbols of the active node at depth d, bytes),
     // U[d] (partial sums of the finished left child at depth d, bits),
     // R (right-chain partial sums, own lane), H (R1 hard decisions),
@@ -408,7 +412,10 @@ __global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t
         wave_sync();
         // best path: first minimum of the path metrics (H6, SCLLUTDecoder.cpp:244)
         int best = 0;
-        if (kList) {
+        if (kList && P.crc_n > 0) {
+            best = ca_winner(pm, gl, gbase, L, P.N, P.info_mask, P.ca_A, P.K, P.crc_n, P.crc_q,
+                             [&](int w) { return row_ptr(wsc, P.Ro + w)[lane]; });
+        } else if (kList) {
             double bpm = shfld(pm, gbase);
             for (int j = 1; j < L; ++j) {
                 const double pj = shfld(pm, gbase + j);
@@ -420,9 +427,9 @@ __global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t
         }
         if (frame_ok) {
             const uint32_t *rb = row_ptr(wsc, P.Ro);
-            for (int t = gl; t < P.K; t += gs) {
+            for (int t = gl; t < P.out_k; t += gs) {
                 const int pos = P.info_pos[t];
-                out[frame * P.K + t] = (uint8_t)((rb[(size_t)(pos >> 5) * 64 + gbase + best] >> (pos & 31)) & 1u);
+                out[frame * P.out_k + t] = (uint8_t)((rb[(size_t)(pos >> 5) * 64 + gbase + best] >> (pos & 31)) & 1u);
             }
         }
         wave_sync();

@@ -48,6 +48,8 @@ __host__ __device__ inline Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint3
 
 struct McChannel {
     int32_t N, K, q, n_edges;
+    int32_t A, crc_n;  // crc_n > 0: A message bits + first K-A bits of their CRC
+    uint32_t crc_q;    // CRC register taps (coefficients 1..crc_n, as ca_winner)
     uint32_t seed_lo, seed_hi;
     float sigma, llr_scale;  // AWGN std and 2/sigma^2
     const int32_t *info_pos; // [K] information positions, ascending
@@ -66,14 +68,25 @@ __global__ __launch_bounds__(64) void mc_frames_kernel(McChannel C, int64_t fram
         const uint32_t glo = (uint32_t)gid, ghi = (uint32_t)(gid >> 32);
         for (int e = t; e < N; e += 64) ux[e] = 0;
         __syncthreads();
-        for (int w = t; w * 128 < K; w += 64) {
+        const int A = C.A;  // message bits (= K without CRC)
+        for (int w = t; w * 128 < A; w += 64) {
             const Philox4 r = philox4x32_10(glo, ghi, (uint32_t)w, kTagMsg, C.seed_lo, C.seed_hi);
-            for (int b = 0; b < 128 && 128 * w + b < K; ++b) {
+            for (int b = 0; b < 128 && 128 * w + b < A; ++b) {
                 const uint8_t bit = (r.v[b >> 5] >> (b & 31)) & 1u;
                 const int j = 128 * w + b;
-                msg_out[f * K + j] = bit;
+                msg_out[f * A + j] = bit;
                 ux[C.info_pos[j]] = bit;
             }
+        }
+        __syncthreads();
+        if (C.crc_n > 0 && t == 0) {  // CRC::encoding (utils.cpp:77-92) as a register, one lane
+            const uint32_t top = 1u << (C.crc_n - 1), mask = (top << 1) - 1u;
+            uint32_t r = 0;
+            for (int j = 0; j < A; ++j) {
+                const uint32_t fb = (uint32_t)ux[C.info_pos[j]] ^ ((r & top) ? 1u : 0u);
+                r = ((r << 1) & mask) ^ (C.crc_q & (0u - fb));
+            }
+            for (int j = 0; j < K - A; ++j) ux[C.info_pos[A + j]] = (uint8_t)((r >> (C.crc_n - 1 - j)) & 1u);
         }
         __syncthreads();
         for (int m = 1; m < N; m *= 2) {  // x = u F^{(x)n}

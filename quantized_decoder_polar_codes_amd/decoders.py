@@ -21,7 +21,13 @@ import numpy as np
 from . import _lib
 from .lut import PackedLUT, pack_luts
 
-__all__ = ["SCDecoder", "SCLUTDecoder", "SCLLUTDecoder", "FastSCLUTDecoder", "FastSCLLUTDecoder"]
+__all__ = ["SCDecoder", "SCLUTDecoder", "SCLLUTDecoder", "FastSCLUTDecoder", "FastSCLLUTDecoder",
+           "CASCLLUTDecoder", "CAFastSCLLUTDecoder"]
+
+# The CRC the reference CA decoders actually check (CASCLLUTDecoder.h:33-34,
+# CAFastSCLLUTDecoder.h:29-30): CRC-24 with these coefficient indices, whatever
+# crc_n / crc_p the CASCLLUTDecoder constructor receives (decode never reads them).
+CRC24_LOC = (24, 23, 21, 20, 17, 15, 13, 12, 8, 4, 2, 1, 0)
 
 
 def _as_i32(x) -> np.ndarray:
@@ -46,10 +52,13 @@ class _DecoderBase:
     _float_input = False
 
     def __init__(self, N, K, L, frozen_bits, message_bits, node_type, packed: PackedLUT | None, device=None,
-                 max_waves: int = 0, engine: str = "auto"):
+                 max_waves: int = 0, engine: str = "auto", A: int | None = None, crc_n: int = 24,
+                 crc_loc=CRC24_LOC):
         self.N = int(N)
         self.K = int(K)
         self.L = int(L)
+        self.A = self.K if A is None else int(A)
+        self.out_bits = self.A
         frozen = _as_i32(frozen_bits).reshape(-1)
         if frozen.size != self.N:
             raise ValueError(f"frozen_bits must have N={self.N} entries, got {frozen.size}")
@@ -83,6 +92,10 @@ class _DecoderBase:
         cfg.max_waves = int(max_waves)
         cfg.engine = {"auto": _lib.QPD_ENGINE_AUTO, "generic": _lib.QPD_ENGINE_GENERIC,
                       "fast": _lib.QPD_ENGINE_FAST}[engine]
+        self._crc_loc = np.ascontiguousarray(np.asarray(crc_loc, dtype=np.int32))
+        if self._kind in (_lib.QPD_CASCL_LUT, _lib.QPD_CAFASTSCL_LUT):
+            cfg.A, cfg.crc_n = self.A, int(crc_n)
+            cfg.crc_loc, cfg.crc_loc_count = _ptr(self._crc_loc), self._crc_loc.size
         h = ctypes.c_void_p()
         _lib.check(lib.qpd_create(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
@@ -113,14 +126,15 @@ class _DecoderBase:
 
     def decode_batch(self, x):
         """Decode B frames.  numpy [B, N] -> numpy uint8 [B, K] (synchronous);
-        torch CUDA tensor [B, N] -> torch CUDA uint8 [B, K] on the current stream."""
+        torch CUDA tensor [B, N] -> torch CUDA uint8 [B, K] on the current stream.
+        (A instead of K for the CRC-aided decoders.)"""
         torch = _torch()
         lib = _lib.load()
         if torch is not None and isinstance(x, torch.Tensor) and x.is_cuda:
             want = torch.float64 if self._float_input else torch.int32
             xs = x.reshape(-1, self.N).to(want).contiguous()
             B = xs.shape[0]
-            out = torch.empty((B, self.K), dtype=torch.uint8, device=xs.device)
+            out = torch.empty((B, self.out_bits), dtype=torch.uint8, device=xs.device)
             stream = torch.cuda.current_stream(xs.device).cuda_stream
             fn = lib.qpd_decode_f64 if self._float_input else lib.qpd_decode
             _lib.check(fn(self._h, ctypes.c_void_p(xs.data_ptr()), B, ctypes.c_void_p(out.data_ptr()),
@@ -131,7 +145,7 @@ class _DecoderBase:
         a = np.asarray(x)
         a = np.ascontiguousarray(a.astype(np.float64 if self._float_input else np.int32).reshape(-1, self.N))
         B = a.shape[0]
-        out = np.empty((B, self.K), dtype=np.uint8)
+        out = np.empty((B, self.out_bits), dtype=np.uint8)
         fn = lib.qpd_decode_f64_host if self._float_input else lib.qpd_decode_host
         _lib.check(fn(self._h, _ptr(a), B, _ptr(out)))
         return out
@@ -189,6 +203,30 @@ class FastSCLLUTDecoder(_LUTDecoder):
                          pack_luts(int(N), LUT_f, LUT_g, virtual_channel_llr), **kw)
 
 
+class CASCLLUTDecoder(_LUTDecoder):
+    """CRC-aided SCL-LUT (CASCLLUTDecoder.cpp:64-303; ctor py_CASCLLUTDecoder.cpp:10-17).
+    ``decode`` returns the A message bits.  Like the reference, ``crc_n``/``crc_p``
+    are accepted and stored but the check is always CRC-24 (CRC24_LOC)."""
+
+    _kind = _lib.QPD_CASCL_LUT
+
+    def __init__(self, N, K, A, L, frozen_bits, message_bits, crc_n, crc_p, LUT_f, LUT_g, virtual_channel_llr, **kw):
+        self.crc_n, self.crc_p = crc_n, crc_p
+        super().__init__(N, K, L, frozen_bits, message_bits, None, pack_luts(int(N), LUT_f, LUT_g, virtual_channel_llr),
+                         A=A, **kw)
+
+
+class CAFastSCLLUTDecoder(_LUTDecoder):
+    """CRC-aided FastSCL-LUT (CAFastSCLLUTDecoder.cpp:58-454; ctor
+    py_CAFastSCLLUTDecoder.cpp:10-16).  ``decode`` returns the A message bits."""
+
+    _kind = _lib.QPD_CAFASTSCL_LUT
+
+    def __init__(self, N, K, A, L, frozen_bits, message_bits, node_type, LUT_f, LUT_g, virtual_channel_llr, **kw):
+        super().__init__(N, K, L, frozen_bits, message_bits, node_type,
+                         pack_luts(int(N), LUT_f, LUT_g, virtual_channel_llr), A=A, **kw)
+
+
 class SCDecoder(_DecoderBase):
     """Float SC, min-sum on float64 LLRs (SCDecoder.cpp:14-89)."""
 
@@ -205,8 +243,10 @@ class SCDecoder(_DecoderBase):
 def from_packed(kind: str, packed: PackedLUT, K: int, frozen_bits, L: int = 1, node_type=None, **kw):
     """Build a decoder directly from packed tables (skips the nested-list path)."""
     cls = {"SC-LUT": SCLUTDecoder, "SCL-LUT": SCLLUTDecoder, "FastSC-LUT": FastSCLUTDecoder,
-           "FastSCL-LUT": FastSCLLUTDecoder}[kind]
+           "FastSCL-LUT": FastSCLLUTDecoder, "CA-SCL-LUT": CASCLLUTDecoder,
+           "CA-FastSCL-LUT": CAFastSCLLUTDecoder}[kind]
     obj = cls.__new__(cls)
-    _DecoderBase.__init__(obj, packed.N, K, L if kind in ("SCL-LUT", "FastSCL-LUT") else 1, frozen_bits,
-                          1 - np.asarray(frozen_bits), node_type, packed, **kw)
+    lst = kind in ("SCL-LUT", "FastSCL-LUT", "CA-SCL-LUT", "CA-FastSCL-LUT")
+    _DecoderBase.__init__(obj, packed.N, K, L if lst else 1, frozen_bits, 1 - np.asarray(frozen_bits), node_type, packed,
+                          **kw)
     return obj

@@ -76,7 +76,7 @@ class GpuFrames:
 
     def __call__(self, frame0: int, B: int):
         torch = self.torch
-        msg = torch.empty((B, self.dec.K), dtype=torch.uint8, device=self.device)
+        msg = torch.empty((B, self.dec.out_bits), dtype=torch.uint8, device=self.device)
         sym = torch.empty((B, self.dec.N), dtype=torch.int32, device=self.device)
         stream = torch.cuda.current_stream(self.device).cuda_stream
         _lib.check(_lib.load().qpd_mc_frames(self.dec._h, ctypes.byref(self.ch), ctypes.c_uint64(self.seed), frame0, B,
@@ -168,8 +168,10 @@ def simulate(decoder, msgbits_count: int, ebn0_list, *, seed: int = 2024, batch:
     out = []
     for eb in ebn0_list:
         src = GpuFrames(decoder, edges, lut, q, sigma_for(eb, rate), point_seed(seed, eb))
-        res = run_point(src, decoder.decode_batch, decoder.K, eb, batch, max_blocks, stop_blkerrs, group=group,
-                        count_device=src.device)
+        # CRC-aided decoders output A bits: errors are counted over A, and the
+        # driver's BER denominators are A (early stop) / K (MaxBlock), :185,196
+        res = run_point(src, decoder.decode_batch, decoder.K, eb, batch, max_blocks, stop_blkerrs, A=decoder.out_bits,
+                        group=group, count_device=src.device)
         torch.cuda.synchronize()
         out.append(res)
     return out

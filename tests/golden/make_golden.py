@@ -94,6 +94,43 @@ def make_lut_case(R, name, kind, N, K, L, lut_kind, B, ebn0, seed):
     print(f"{name:28s} {kind:12s} N={N} K={K} L={L} B={B} ref {dt:.1f}s  BLER={errs:.3f}")
 
 
+def make_ca_case(R, name, kind, N, A, L, lut_kind, B, ebn0, seed, crc_n=24):
+    """CRC-aided list decoders: A message bits + CRC-24 (the check the reference's
+    CA decoders hard-code, CASCLLUTDecoder.h:33-34), K = A + crc_n."""
+    rng = np.random.default_rng(seed)
+    K = A + crc_n
+    _, msgbits, frozen, msgmask = C.construct_pw(N, K)
+    node_type = C.identify_nodes(N, msgbits).astype(np.int32)
+    v, delta = 16, 0.5
+    packed = LU.minsum_uniform_luts(N, v=v, delta=delta) if lut_kind == "minsum" else \
+        LU.random_luts(N, v=v, seed=seed, distinct_mags=4)
+    msg = rng.integers(0, 2, size=(B, A), dtype=np.uint8)
+    u = np.concatenate([msg, O.crc_encode(msg, crc_n, O.CRC24_LOC)], axis=1)
+    x = C.polar_encode(u, msgbits, N)
+    sigma = np.sqrt(1 / (2 * (K / N) * 10 ** (ebn0 / 10)))
+    llr = ((1.0 - 2.0 * x) + rng.normal(0, sigma, size=(B, N))) * 2 / sigma ** 2
+    sym = uniform_channel_symbols(llr, v, delta)
+    fs, gs, vcl = LU.unpack_to_reference(packed)
+    fz, mm = frozen.astype(int).tolist(), msgmask.astype(int).tolist()
+    if kind == "CA-SCL-LUT":
+        d = R.CASCLLUTDecoder(N, K, A, L, fz, mm, crc_n, list(O.CRC24_LOC), fs, gs, vcl)
+    else:
+        d = R.CAFastSCLLUTDecoder(N, K, A, L, fz, mm, node_type.tolist(), fs, gs, vcl)
+    t = time.time()
+    out = np.stack([d.decode(s.astype(np.int32)) for s in sym]).astype(np.uint8)
+    dt = time.time() - t
+    np.savez_compressed(
+        os.path.join(HERE, name + ".npz"),
+        kind=kind, N=N, K=K, A=A, L=L, v=v, crc_n=crc_n, crc_loc=np.array(O.CRC24_LOC, dtype=np.int8),
+        lut_kind=lut_kind, ebn0_db=ebn0, seed=seed,
+        frozen=frozen.astype(np.int8), node_type=node_type.astype(np.int8),
+        lut_f=packed.lut_f, f_base=packed.f_base, f_step=packed.f_step,
+        lut_g=packed.lut_g, g_base=packed.g_base, g_step=packed.g_step,
+        vcl=packed.vcl, msg=msg, symbols=sym.astype(np.uint8), expected=out,
+    )
+    print(f"{name:28s} {kind:14s} N={N} K={K} A={A} L={L} B={B} ref {dt:.1f}s  BLER={(out != msg).any(1).mean():.3f}")
+
+
 def make_float_case(R, name, N, K, B, ebn0, seed):
     rng = np.random.default_rng(seed)
     _, msgbits, frozen, msgmask = C.construct_pw(N, K)
@@ -122,5 +159,20 @@ def main():
     make_lut_case(R, "sclut_n1024_k512_minsum", "SC-LUT", 1024, 512, 1, "minsum", 300, 2.0, 10)
 
 
+def main_ca():
+    R = O.reference_module()
+    if R is None:
+        raise SystemExit("oracle/_ref not built (run oracle/build_ref.sh)")
+    make_ca_case(R, "ca_scllut_n128_a40_l8_minsum", "CA-SCL-LUT", 128, 40, 8, "minsum", 600, 1.5, 11)
+    make_ca_case(R, "ca_fastscllut_n128_a40_l8_minsum", "CA-FastSCL-LUT", 128, 40, 8, "minsum", 600, 1.5, 12)
+    make_ca_case(R, "ca_scllut_n128_a40_l4_random", "CA-SCL-LUT", 128, 40, 4, "random", 300, 1.5, 13)
+    make_ca_case(R, "ca_scllut_n1024_a488_l8_minsum", "CA-SCL-LUT", 1024, 488, 8, "minsum", 150, 1.5, 14)
+    make_ca_case(R, "ca_fastscllut_n1024_a488_l8_minsum", "CA-FastSCL-LUT", 1024, 488, 8, "minsum", 150, 1.5, 15)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["ca"]:
+        main_ca()  # only the CRC-aided fixtures
+    else:
+        main()
+        main_ca()

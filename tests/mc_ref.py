@@ -25,19 +25,27 @@ def philox(c0, c1, c2, c3, k0, k1):
     return c0, c1, c2, c3
 
 
-def frames(N, K, msgbits, seed, frame0, B, sigma, edges, lut, q):
+def frames(N, K, msgbits, seed, frame0, B, sigma, edges, lut, q, A=None, crc=None):
+    """crc = (crc_n, loc): the message is A bits followed by the first K-A bits of
+    their CRC (oracle.crc_encode, the reference's CRC::encoding); returns the A bits."""
+    A = K if A is None else A
     gid = np.arange(frame0, frame0 + B, dtype=np.uint64)
     glo, ghi = gid & np.uint64(MASK), gid >> np.uint64(32)
     slo, shi = seed & MASK, (seed >> 32) & MASK
-    msg = np.zeros((B, K), dtype=np.uint8)
-    for w in range((K + 127) // 128):
+    msg = np.zeros((B, A), dtype=np.uint8)
+    for w in range((A + 127) // 128):
         r = philox(glo, ghi, np.full(B, w, np.uint64), np.full(B, TAG_MSG, np.uint64), slo, shi)
         for b in range(128):
             j = 128 * w + b
-            if j >= K:
+            if j >= A:
                 break
             msg[:, j] = ((r[b >> 5] >> np.uint64(b & 31)) & np.uint64(1)).astype(np.uint8)
-    x = C.polar_encode(msg, msgbits, N)
+    u = msg
+    if crc is not None:
+        import oracle
+
+        u = np.concatenate([msg, oracle.crc_encode(msg, crc[0], crc[1])[:, : K - A]], axis=1)
+    x = C.polar_encode(u, msgbits, N)
     llr = np.zeros((B, N), dtype=np.float64)
     for p in range(N // 2):
         r = philox(glo, ghi, np.full(B, p, np.uint64), np.full(B, TAG_NOISE, np.uint64), slo, shi)

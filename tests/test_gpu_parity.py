@@ -53,8 +53,9 @@ def test_gpu_matches_golden(path, engine, qpd):
         dec = qpd.SCDecoder(N, K, g["frozen"], 1 - g["frozen"])
         got = dec.decode_batch(g["llr"])
     else:
+        kw = {"A": int(g["A"])} if str(g["kind"]).startswith("CA-") else {}
         dec = qpd.from_packed(str(g["kind"]), golden_packed(g), K, g["frozen"], L=L, node_type=g["node_type"],
-                              engine=engine)
+                              engine=engine, **kw)
         assert dec.info()["engine"] == (2 if engine == "auto" else 1)
         got = dec.decode_batch(g["symbols"].astype(np.int32))
     bad = np.flatnonzero((got != g["expected"]).any(1))
@@ -108,6 +109,82 @@ def test_gpu_matches_oracle(N, K, L, tables, kind, engine, qpd, oracle_mod):
     got = dec.decode_batch(sym)
     bad = np.flatnonzero((got != want).any(1))
     assert bad.size == 0, f"{bad.size}/{B} frames differ, first {bad[:5]}"
+
+
+CA_CASES = [
+    # N, A, crc_n, L, tables, Eb/N0
+    (32, 6, 24, 2, "minsum", 3.0),
+    (64, 20, 24, 4, "minsum", 2.0),
+    (128, 40, 24, 8, "minsum", 1.0),
+    (128, 40, 24, 8, "random", 1.0),
+    (256, 100, 11, 8, "minsum", 1.5),   # a shorter CRC (5G CRC11 taps)
+    (512, 230, 24, 3, "minsum", 1.5),
+    (1024, 488, 24, 8, "minsum", 1.5),
+    (1024, 500, 24, 8, "minsum", 1.5),  # K - A = 12 < crc_n: only the first 12 check bits compared
+]
+CRC11_LOC = (11, 10, 9, 5, 0)
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+@pytest.mark.parametrize("N,A,crc_n,L,tables,ebn0", CA_CASES)
+@pytest.mark.parametrize("kind", ["CA-SCL-LUT", "CA-FastSCL-LUT"])
+def test_gpu_ca_matches_oracle(N, A, crc_n, L, tables, ebn0, kind, engine, qpd, oracle_mod):
+    """CRC-aided decoders on frames that carry a real CRC, so the CRC decides
+    the output path on many frames (checked below)."""
+    from quantized_decoder_polar_codes_amd import codes as C
+    from quantized_decoder_polar_codes_amd import lut as LU
+
+    loc = oracle_mod.CRC24_LOC if crc_n == 24 else CRC11_LOC
+    K = 512 if (N, A) == (1024, 500) else A + crc_n
+    seed = 5000 + N + A + L
+    _, mb, fm, mm = C.construct_pw(N, K)
+    nt = C.identify_nodes(N, mb).astype(np.int32)
+    p = LU.minsum_uniform_luts(N) if tables == "minsum" else LU.random_luts(N, 16, seed=seed, distinct_mags=3)
+    rng = np.random.default_rng(seed)
+    B = 48 if N >= 1024 else 300
+    msg = rng.integers(0, 2, size=(B, A), dtype=np.uint8)
+    u = np.concatenate([msg, oracle_mod.crc_encode(msg, crc_n, loc)[:, : K - A]], axis=1)
+    x = C.polar_encode(u, mb, N)
+    sigma = np.sqrt(1 / (2 * (K / N) * 10 ** (ebn0 / 10)))
+    llr = ((1.0 - 2.0 * x) + rng.normal(0, sigma, size=(B, N))) * 2 / sigma ** 2
+    sym = np.clip(np.rint(llr / 0.5 + 7.5), 0, 15).astype(np.int32)
+    special_root = kind == "CA-FastSCL-LUT" and 0 <= nt[0] <= 2
+    if special_root:
+        with pytest.raises(ValueError):
+            qpd.from_packed(kind, p, K, fm, L=L, node_type=nt, engine=engine, A=A, crc_n=crc_n, crc_loc=loc)
+        return
+    want = oracle_mod.decode_lut_ca(kind, p, K, A, L, fm, sym, node_type=nt, crc_n=crc_n, crc_loc=loc)
+    dec = qpd.from_packed(kind, p, K, fm, L=L, node_type=nt, engine=engine, A=A, crc_n=crc_n, crc_loc=loc)
+    assert dec.info()["out_bits"] == A
+    got = dec.decode_batch(sym)
+    assert got.shape == (B, A)
+    bad = np.flatnonzero((got != want).any(1))
+    assert bad.size == 0, f"{bad.size}/{B} frames differ, first {bad[:5]}"
+
+
+def test_ca_dropin_api(qpd, oracle_mod):
+    """The reference's constructor order / kwargs and one-frame decode()."""
+    from PolarDecoder.Decoder.CAFastSCLLUTDecoder import CAFastSCLLUTDecoder
+    from PolarDecoder.Decoder.CASCLLUTDecoder import CASCLLUTDecoder
+    from quantized_decoder_polar_codes_amd import codes as C
+    from quantized_decoder_polar_codes_amd import lut as LU
+
+    N, A, L = 128, 40, 8
+    K = A + 24
+    _, mb, fm, mm = C.construct_pw(N, K)
+    nt = C.identify_nodes(N, mb).astype(np.int32)
+    p = LU.minsum_uniform_luts(N)
+    fs, gs, vcl = LU.unpack_to_reference(p)
+    sym = np.random.default_rng(3).integers(2, 14, size=(5, N), dtype=np.int32)
+    d0 = CASCLLUTDecoder(N, K, A, L, fm.tolist(), mm.tolist(), 24, list(oracle_mod.CRC24_LOC), fs, gs, vcl)
+    d1 = CAFastSCLLUTDecoder(N=N, K=K, A=A, L=L, frozen_bits=fm, message_bits=mm, node_type=nt, LUT_f=fs,
+                                LUT_g=gs, virtual_channel_llr=vcl)
+    for d, kind in ((d0, "CA-SCL-LUT"), (d1, "CA-FastSCL-LUT")):
+        want = oracle_mod.decode_lut_ca(kind, p, K, A, L, fm, sym, node_type=nt)
+        for i in range(len(sym)):
+            out = d.decode(sym[i][None])
+            assert out.dtype == np.uint8 and out.shape == (A,)
+            assert np.array_equal(out, want[i])
 
 
 def test_sc_float_matches_oracle(qpd, oracle_mod):

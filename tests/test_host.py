@@ -124,7 +124,9 @@ def test_library_exports_every_declared_symbol(native_lib):
     assert set(declared) == set(_lib.EXPORTED)
     for name in declared:
         assert hasattr(native_lib, name), name
-    assert native_lib.qpd_abi_version() == 1
+    txt = open(os.path.join(ROOT, "include", "qpd.h")).read()
+    ver = int(re.search(r"#define QPD_ABI_VERSION (\d+)", txt).group(1))
+    assert native_lib.qpd_abi_version() == ver == _lib.ABI_VERSION
 
 
 def _cfg(kind=2, N=8, K=4, L=4, frozen=None, over=None):
@@ -163,6 +165,36 @@ def test_create_rejects_bad_config(native_lib, over, code):
     rc = native_lib.qpd_create(ctypes.byref(c), ctypes.byref(h))
     assert rc == code
     assert native_lib.qpd_last_error()
+
+
+@pytest.mark.parametrize("over", [
+    {"A": 0, "crc_n": 24},               # A outside [1, K]
+    {"A": 5, "crc_n": 24},
+    {"A": 2, "crc_n": 0},                # crc_n outside [1, 32]
+    {"A": 2, "crc_n": 33},
+    {"A": 1, "crc_n": 2},                # K - A > crc_n (reference reads past its check code)
+    {"A": 2, "crc_n": 24, "crc_loc_count": 1},  # crc_loc count without pointer
+])
+def test_create_rejects_bad_crc_config(native_lib, over):
+    from quantized_decoder_polar_codes_amd import _lib
+
+    for kind in (_lib.QPD_CASCL_LUT, _lib.QPD_CAFASTSCL_LUT):
+        c, keep = _cfg(kind=kind, over=over)
+        nt = -np.ones(15, dtype=np.int32)
+        c.node_type = nt.ctypes.data
+        h = ctypes.c_void_p()
+        assert native_lib.qpd_create(ctypes.byref(c), ctypes.byref(h)) == -1
+        assert native_lib.qpd_last_error()
+
+
+def test_create_rejects_crc_loc_out_of_range(native_lib):
+    from quantized_decoder_polar_codes_amd import _lib
+
+    loc = np.array([24, 25, 0], dtype=np.int32)
+    c, keep = _cfg(kind=_lib.QPD_CASCL_LUT, over={"A": 2, "crc_n": 24, "crc_loc": loc.ctypes.data,
+                                                  "crc_loc_count": 3})
+    h = ctypes.c_void_p()
+    assert native_lib.qpd_create(ctypes.byref(c), ctypes.byref(h)) == -1
 
 
 def test_create_rejects_special_root(native_lib):

@@ -16,6 +16,9 @@ def test_oracle_matches_golden(path, oracle_mod):
     N, K, L = int(g["N"]), int(g["K"]), int(g["L"])
     if str(g["kind"]) == "SC":
         got = oracle_mod.decode_sc_float(N, K, g["frozen"], g["llr"])
+    elif str(g["kind"]).startswith("CA-"):
+        got = oracle_mod.decode_lut_ca(str(g["kind"]), golden_packed(g), K, int(g["A"]), L, g["frozen"],
+                                       g["symbols"].astype(np.int32), node_type=g["node_type"])
     else:
         got = oracle_mod.decode_lut(str(g["kind"]), golden_packed(g), K, L, g["frozen"],
                                     g["symbols"].astype(np.int32), node_type=g["node_type"])
