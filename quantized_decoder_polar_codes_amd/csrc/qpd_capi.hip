@@ -688,7 +688,8 @@ int qpd_decode(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_o
         const void *kfn = fast_kernel(d->kind, d->sets, d->l8);
         if (!kfn) return fail(QPD_E_INVALID, "bad kind");
         const int32_t *in_arg = d_symbols;
-        void *args[] = {&fp, &in_arg, &B, &d_out};
+        const qpd::MOp *ops_arg = fp.ops;
+        void *args[] = {&fp, &in_arg, &B, &d_out, &ops_arg};
         QPD_HIP(hipLaunchKernel(kfn, dim3(fgrid), dim3(64), args, lds, st));
         QPD_HIP(hipGetLastError());
         return QPD_OK;

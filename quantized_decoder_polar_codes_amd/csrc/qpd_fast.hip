@@ -519,8 +519,12 @@ __device__ unsigned long long qpd_stamp_acc[64];
 // LDS: NS * kSelInts ints of selection scratch, then NS * lds_rows rows.
 // Global slab: NS * glb_rows rows per workgroup.
 template <int KIND, int NS, bool L8>
+// `ops` is its own __restrict__ argument (= P.ops) so that the compiler can
+// prove the op records are never written and fetch them with scalar loads
+// instead of vector loads + readfirstlane, which drain vmcnt at every op.
 __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : QPD_WPE1) void lut_fast_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
-                                                               uint8_t *__restrict__ out) {
+                                                               uint8_t *__restrict__ out,
+                                                               const MOp *__restrict__ ops) {
     constexpr bool kList = (KIND == K_SCL_LUT || KIND == K_FASTSCL_LUT);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
     int *const sel_all = (int *)lds_dyn;
@@ -554,7 +558,7 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : QPD_WPE1) void lut_fast_ke
 #ifdef QPD_STAMPS
         uint64_t stamp_acc = 0, stamp_cnt = 0;
 #endif
-        MOp nxt = P.ops[0];
+        MOp nxt = ops[0];
         Pre pre = fetch_pre(P, nxt, threadIdx.x, threadIdx.x < P.v ? threadIdx.x : 0);
         for (int oi = 0; oi < P.nops; ++oi) {
             // Re-derive the lane constants every op: without this the compiler
@@ -565,12 +569,13 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : QPD_WPE1) void lut_fast_ke
             const int gl = lane & (gs - 1);
             const int gbase = lane & ~(gs - 1);
             const int vlane = lane < P.v ? lane : 0;
-            const int32_t *yv[NS];
+            const int32_t *yv[NS];  // channel rows (read by MF_CHAN ops only)
+            const int gsh = __builtin_ctz(gs);
 #pragma unroll
             for (int s = 0; s < NS; ++s) {
-                int64_t f = (task * NS + s) * fpw + lane / gs;
+                int64_t f = (task * NS + s) * fpw + (lane >> gsh);
                 if (f >= B) f = B - 1;
-                yv[s] = in + f * (int64_t)N;
+                yv[s] = in + (f << P.n);
             }
             if (nxt.flags & MF_SYNC) wave_sync();  // before the next prefetch is issued
             const MOp op = nxt;
@@ -580,7 +585,7 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : QPD_WPE1) void lut_fast_ke
             const uint64_t stamp_t0 = __builtin_amdgcn_s_memtime();
 #endif
             if (oi + 1 < P.nops) {
-                nxt = P.ops[oi + 1];
+                nxt = ops[oi + 1];
                 pre = fetch_pre(P, nxt, lane, vlane);
             }
             const int fl = op.flags;
