@@ -3,7 +3,12 @@
 Q=16) decoder (BASELINE.json `metric`, configs[2]), 1..8 MI355X.
 
 A step = one decode launch over one batch of synthetic AWGN frames that are
-already resident in HBM.  With --gpus N>1 the driver runs this under
+already resident in HBM.  The workload is the reference driver's
+(mainQuantizedDecoder_LLRDomain.py:130-176): frames from the GPU Monte-Carlo
+generator (qpd_mc_frames: Philox4x32-10 keyed by global frame id, polar
+encoding, BPSK + AWGN at Eb/N0, LLR), the MinDistortion channel quantizer
+designed at that Eb/N0, and MinDistortion decoder tables designed at 3 dB
+(lutgen.py, the reference generator's algorithm).  With --gpus N>1 the driver runs this under
 torch.distributed.run; every rank decodes its own disjoint frame range (weak
 scaling, no collective on the data path) and the only collective is the RCCL
 all-reduce of the error counters {bit errors, block errors, frames}.
@@ -11,7 +16,8 @@ all-reduce of the error counters {bit errors, block errors, frames}.
 Rank 0 prints one JSON line (contract in the task statement), including
 `roofline` for the decode kernel (HIP-event timing on the launch stream) and
 `cpu_baseline` (the reference decoder compiled from its sources, oracle/_ref,
-timed on one host core over a bounded sample of the same workload).
+one worker process per host core of this GPU's CPU share, over a bounded
+sample of the same frames).
 """
 from __future__ import annotations
 
@@ -47,65 +53,104 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--engine", default="auto", choices=["auto", "fast", "generic"])
+    ap.add_argument("--luts", default="mindistortion", choices=["mindistortion", "minsum"],
+                    help="decoder tables: MinDistortion design (lutgen.py) or synthetic saturating min-sum")
+    ap.add_argument("--design-snr", type=float, default=3.0, help="LUT design SNR (dB)")
+    ap.add_argument("--cpu-workers", type=int, default=0, help="0 = this GPU's CPU share (OMP_NUM_THREADS, <= 16)")
     return ap.parse_args()
 
 
-def synth_frames(N, K, frames, ebn0, seed, msgbits, dev, v=16, delta=0.5):
-    """Reference driver channel (mainQuantizedDecoder_LLRDomain.py:132-176), generated
-    on the GPU with torch's counter-based RNG: message bits, polar encoding
-    (x = u F^{(x)n}, the un-vendored PolarEnc restated), BPSK, AWGN at Eb/N0,
-    LLR = 2y/sigma^2 and a uniform 16-level channel quantizer matching the
-    synthetic min-sum tables.  Returns device tensors (msg uint8 [F,K], sym int32 [F,N])."""
-    import torch
-
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed)
-    sigma = float(np.sqrt(1 / (2 * (K / N) * 10 ** (ebn0 / 10))))
-    msg = torch.randint(0, 2, (frames, K), generator=g, device=dev, dtype=torch.uint8)
-    u = torch.zeros((frames, N), dtype=torch.uint8, device=dev)
-    u[:, torch.as_tensor(msgbits, device=dev)] = msg
-    m = 1
-    while m < N:
-        w = u.view(frames, N // (2 * m), 2, m)
-        w[:, :, 0, :] ^= w[:, :, 1, :]
-        m *= 2
-    llr = (1.0 - 2.0 * u.float() + sigma * torch.randn((frames, N), generator=g, device=dev)) * (2 / sigma ** 2)
-    sym = torch.clamp(torch.round(llr / delta + (v - 1) / 2.0), 0, v - 1).to(torch.int32)
-    return msg, sym
-
-
-def cpu_baseline(args, packed, fm, nt, sym, seconds):
-    """Reference decoder (oracle/_ref, compiled from /root/reference sources) on
-    one core; falls back to the oracle restatement (kind "port")."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
+def workload(N, K, L, kind, frames, ebn0, luts="mindistortion", design_snr=3.0, frame0=0, device=None, **dec_kw):
+    """The benchmark workload: (decoder, packed tables, frozen mask, node types,
+    device msg uint8 [F, K], device symbols int32 [F, N]) -- see the module doc."""
+    import quantized_decoder_polar_codes_amd as Q
+    from quantized_decoder_polar_codes_amd import codes as C
     from quantized_decoder_polar_codes_amd import lut as LU
+    from quantized_decoder_polar_codes_amd import lutgen as LG
+    from quantized_decoder_polar_codes_amd import montecarlo as MC
 
-    R = oracle.reference_module()
-    N, K, L = args.N, args.K, args.L
-    if R is not None:
-        fs, gs, vcl = LU.unpack_to_reference(packed)
-        fz, mm = fm.astype(int).tolist(), (1 - fm).astype(int).tolist()
-        ctor = {"SC-LUT": lambda: R.SCLUTDecoder(N, K, fz, mm, fs, gs, vcl),
-                "SCL-LUT": lambda: R.SCLLUTDecoder(N, K, L, fz, mm, fs, gs, vcl),
-                "FastSC-LUT": lambda: R.FastSCLUTDecoder(N, K, fz, mm, nt.tolist(), fs, gs, vcl),
-                "FastSCL-LUT": lambda: R.FastSCLLUTDecoder(N, K, L, fz, mm, nt.tolist(), fs, gs, vcl)}
-        dec = ctor[args.kind]()
-        kind = "reference"
-        one = lambda s: dec.decode(s)  # noqa: E731
+    _, mb, fm, mm = C.construct_pw(N, K)
+    nt = C.identify_nodes(N, mb).astype(np.int32)
+    sigma = MC.sigma_for(ebn0, K / N)  # mainQuantizedDecoder_LLRDomain.py:132-133
+    if luts == "mindistortion":
+        packed = LG.design(N, 16, design_snr).packed()
+        _, _, edges, clut = LG.channel_quantizer(sigma, 128, 16)  # the driver's per-Eb/N0 channel quantizer
     else:
-        kind = "port"
-        one = lambda s: oracle.decode_lut(args.kind, packed, K, L, fm, s[None], node_type=nt)[0]  # noqa: E731
-    outs = []
-    t0 = time.perf_counter()
-    i = 0
-    while time.perf_counter() - t0 < seconds and i < len(sym):
-        outs.append(one(sym[i]))
-        i += 1
-    dt = time.perf_counter() - t0
-    return {"value": i / dt, "unit": "frames/s", "cores": 1, "kind": kind,
-            "sample": f"{i} frames of the same workload (first frames of rank 0's batch), one decode() call per "
-                      f"frame, single thread, {dt:.1f} s"}, np.stack(outs)
+        packed = LU.minsum_uniform_luts(N, v=16, delta=0.5)
+        edges, clut = MC.uniform_channel_quantizer(16, 0.5)
+    dec = Q.from_packed(kind, packed, K, fm, L=L, node_type=nt, device=device, **dec_kw)
+    src = MC.GpuFrames(dec, edges, clut, 16, sigma, seed=1234)  # Philox keyed by global frame id
+    msg, sym = src(frame0, frames)
+    return dec, packed, fm, nt, msg, sym
+
+
+_WORKER = r"""
+import sys, time, json
+import numpy as np
+sys.path.insert(0, ROOT); sys.path.insert(0, ROOT + "/oracle")
+import oracle
+from quantized_decoder_polar_codes_amd import lut as LU
+z = np.load(PATH, allow_pickle=False)
+R = oracle.reference_module()
+N, K, L, kind = int(z["N"]), int(z["K"]), int(z["L"]), str(z["kind"])
+packed = LU.PackedLUT(N=N, v=int(z["v"]), lut_f=z["lut_f"], f_base=z["f_base"], f_step=0, lut_g=z["lut_g"],
+                      g_base=z["g_base"], g_step=0, vcl=np.ascontiguousarray(z["vcl"]))
+fm, nt, sym = z["frozen"], z["node_type"], z["sym"]
+if R is not None:
+    fs, gs, vcl = LU.unpack_to_reference(packed)
+    fz, mm = fm.astype(int).tolist(), (1 - fm).astype(int).tolist()
+    dec = {"SC-LUT": lambda: R.SCLUTDecoder(N, K, fz, mm, fs, gs, vcl),
+           "SCL-LUT": lambda: R.SCLLUTDecoder(N, K, L, fz, mm, fs, gs, vcl),
+           "FastSC-LUT": lambda: R.FastSCLUTDecoder(N, K, fz, mm, nt.tolist(), fs, gs, vcl),
+           "FastSCL-LUT": lambda: R.FastSCLLUTDecoder(N, K, L, fz, mm, nt.tolist(), fs, gs, vcl)}[kind]()
+    one = dec.decode
+else:
+    one = lambda s: oracle.decode_lut(kind, packed, K, L, fm, s[None], node_type=nt)[0]
+outs = []
+t0 = time.perf_counter()
+while time.perf_counter() - t0 < SECONDS and len(outs) < len(sym):
+    outs.append(one(sym[len(outs)]))
+dt = time.perf_counter() - t0
+np.save(PATH + ".out.npy", np.stack(outs).astype(np.uint8))
+print(json.dumps({"frames": len(outs), "seconds": dt, "kind": "reference" if R is not None else "port"}))
+"""
+
+
+def cpu_baseline(args, packed, fm, nt, sym, seconds, workers):
+    """The reference decoder (oracle/_ref, compiled from /root/reference sources;
+    the oracle restatement, kind "port", if that build is absent), one worker
+    process per core, each decoding its own slice of the sample one frame per
+    decode() call for `seconds`.  Workers are plain child processes (no GPU)."""
+    import subprocess
+    import tempfile
+
+    per = len(sym) // workers
+    tmp = tempfile.mkdtemp(prefix="qpd_cpu_")
+    procs = []
+    for w in range(workers):
+        path = os.path.join(tmp, f"w{w}.npz")
+        np.savez(path, N=args.N, K=args.K, L=args.L, kind=args.kind, v=packed.v, lut_f=packed.lut_f,
+                 f_base=packed.f_base, lut_g=packed.lut_g, g_base=packed.g_base, vcl=packed.vcl, frozen=fm,
+                 node_type=nt, sym=sym[w * per:(w + 1) * per])
+        code = _WORKER.replace("ROOT", repr(ROOT)).replace("PATH", repr(path)).replace("SECONDS", repr(seconds))
+        procs.append((subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True), path))
+    total, walls, outs, kind = 0, [], [], "port"
+    for w, (p, path) in enumerate(procs):
+        o, _ = p.communicate()
+        if p.returncode != 0:
+            raise RuntimeError(f"cpu baseline worker {w} failed")
+        r = json.loads(o.strip().splitlines()[-1])
+        total += r["frames"]
+        walls.append(r["seconds"])
+        kind = r["kind"]
+        outs.append((w * per, np.load(path + ".out.npy")))
+    import shutil
+
+    shutil.rmtree(tmp, ignore_errors=True)
+    wall = max(walls)
+    return {"value": total / wall, "unit": "frames/s", "cores": workers, "kind": kind,
+            "sample": f"{total} frames of the same workload (rank 0's first frames), {workers} worker processes x "
+                      f"one decode() call per frame, {wall:.1f} s"}, outs
 
 
 def main():
@@ -123,19 +168,13 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    import quantized_decoder_polar_codes_amd as Q
-    from quantized_decoder_polar_codes_amd import codes as C
-    from quantized_decoder_polar_codes_amd import lut as LU
-
     N, K, L = args.N, args.K, args.L
-    _, mb, fm, mm = C.construct_pw(N, K)
-    nt = C.identify_nodes(N, mb).astype(np.int32)
-    packed = LU.minsum_uniform_luts(N, v=16, delta=0.5)
-    dec = Q.from_packed(args.kind, packed, K, fm, L=L, node_type=nt, device=dev.index, max_waves=args.max_waves,
-                        engine=args.engine)
+    # rank r owns global frames [r*F, (r+1)*F) of one Philox stream
+    dec, packed, fm, nt, d_msg, d_sym = workload(N, K, L, args.kind, args.frames, args.ebn0, args.luts, args.design_snr,
+                                                 frame0=rank * args.frames, device=dev.index,
+                                                 max_waves=args.max_waves, engine=args.engine)
     info = dec.info()
-    # rank r owns global frames [r*F, (r+1)*F): seed by rank -> disjoint frame sets
-    d_msg, d_sym = synth_frames(N, K, args.frames, args.ebn0, 1234 + rank, mb, dev)
+    torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
 
     out = None
@@ -197,11 +236,14 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic, generated on the GPU (torch Philox): random messages, polar-encoded, BPSK + AWGN at Eb/N0 below, uniform 16-level channel quantizer, "
-                    "synthetic saturating min-sum 16-level LUTs; resident in HBM",
+            "data": ("synthetic, generated on the GPU by qpd_mc_frames (Philox4x32-10 keyed by global frame id): random "
+                     "messages, polar-encoded, BPSK + AWGN at Eb/N0 below, the driver's MinDistortion channel quantizer "
+                     f"(128 -> 16 levels); decoder tables: {args.luts}"
+                     + (f" designed at {args.design_snr:g} dB by lutgen.py" if args.luts == "mindistortion" else "")
+                     + "; resident in HBM"),
             "config": {"workload": f"{args.kind} N={N} K={K} L={L} Q=16 (5G-NR PW code, no CRC)",
                        "decoder": args.kind, "N": N, "K": K, "L": L, "v": 16, "frames_per_gpu_per_step": args.frames,
-                       "ebn0_db": args.ebn0, "parallelism": f"dp{world} (frames sharded, RCCL counter all-reduce)",
+                       "ebn0_db": args.ebn0, "luts": args.luts, "parallelism": f"dp{world} (frames sharded, RCCL counter all-reduce)",
                        "engine": {1: "generic", 2: "fast"}[info["engine"]], "lds_bytes_per_wave": info["lds_bytes_per_wave"],
                        "lds_from_depth": info["lds_from_depth"], "waves": min(info["max_waves"],
                        -(-args.frames // info["frames_per_wave"]))},
@@ -215,12 +257,13 @@ def main():
                                               "bytes_per_frame": LOOKUPS_PER_FRAME * ONCHIP_BYTES_PER_LOOKUP}},
         }
         if world == 1 and not args.no_cpu_baseline:
-            sample = d_sym[:4096].cpu().numpy()
-            cb, ref_out = cpu_baseline(args, packed, fm, nt, sample, args.cpu_baseline_seconds)
+            workers = args.cpu_workers or min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+            sample = d_sym[: 1 << 15].cpu().numpy()
+            cb, parts = cpu_baseline(args, packed, fm, nt, sample, args.cpu_baseline_seconds, max(1, workers))
             res["cpu_baseline"] = cb
-            gpu_out = out[: len(ref_out)].cpu().numpy()
-            res["parity_sample"] = {"frames": int(len(ref_out)),
-                                    "bit_exact_vs_" + cb["kind"]: bool((gpu_out == ref_out).all())}
+            gpu_out = out.cpu().numpy()
+            ok = all(np.array_equal(gpu_out[o:o + len(r)], r) for o, r in parts)
+            res["parity_sample"] = {"frames": int(sum(len(r) for _, r in parts)), "bit_exact_vs_" + cb["kind"]: bool(ok)}
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -162,6 +162,36 @@ typedef struct qpd_mc_channel {
 int qpd_mc_frames(qpd_decoder *dec, const qpd_mc_channel *ch, uint64_t seed, int64_t frame0, int64_t B,
                   uint8_t *d_msg, int32_t *d_symbols, void *stream);
 
+/*
+ * Offline table design (host code, no device needed) -- the reference's
+ * MinDistortion LUT generator without OpenCV.
+ *
+ * qpd_optls_quantizer  <- LLRQuantizer::find_OptLS_quantizer
+ *                         Quantizers/quantizers/_cpp/LLRQuantizer/LLRQuantizer.cpp:67-165
+ *                         (Python twin QuantizeDensityEvolution/MinDistortionQuantizer.py:28-99):
+ *   merge M LLR quanta (any order; density-weighted) into K groups of
+ *   consecutive sorted quanta with minimum squared error.  Outputs
+ *   density[K], quanta[K] (density-weighted means), lut[M] (symbol -> group)
+ *   and the minimum distortion.
+ * qpd_lutgen_mindistortion <- LLRQuantizerSC.run
+ *                         QuantizeDensityEvolution/QLLRDensityEvolution_MinDistortion.py:73-126:
+ *   density evolution of the v-level channel (density/quanta [v]) down the
+ *   code tree; per node p = 2^depth + node - 1 one f table lut_f[p][a][b] and
+ *   one g table lut_g[p][u][a][b] (uint8, [N-1][v][v] / [N-1][2][v][v]), and
+ *   the evolved llr_density / llr_quanta [log2(N)+1][N][v] (llr_quanta is
+ *   the decoders' virtual_channel_llr).  threads <= 0: all host cores.
+ * sum_order: QPD_SUM_SEQUENTIAL = the C++ quantizer the reference generator
+ * calls; QPD_SUM_NUMPY = its numpy twin (pairwise sums).  Returns 0, -1 on bad
+ * arguments, -2 if a node has fewer than v distinct values (the reference
+ * aborts there: CV_Assert(M >= K)).
+ */
+enum qpd_sum_order { QPD_SUM_SEQUENTIAL = 0, QPD_SUM_NUMPY = 1 };
+int qpd_optls_quantizer(const double *density, const double *quanta, int32_t M, int32_t K, int32_t sum_order,
+                        double *out_density, double *out_quanta, int32_t *out_lut, double *out_distortion);
+int qpd_lutgen_mindistortion(int32_t N, int32_t v, const double *ch_density, const double *ch_quanta,
+                             int32_t sum_order, int32_t threads, uint8_t *lut_f, uint8_t *lut_g,
+                             double *llr_density, double *llr_quanta);
+
 /* Introspection for tests / benchmarks. */
 typedef struct qpd_info {
     int32_t kind, N, K, L, v;

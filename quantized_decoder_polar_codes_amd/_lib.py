@@ -30,6 +30,8 @@ EXPORTED = (
     "qpd_check_input_error",
     "qpd_get_info",
     "qpd_mc_frames",
+    "qpd_optls_quantizer",
+    "qpd_lutgen_mindistortion",
 )
 
 _P = ctypes.c_void_p
@@ -142,6 +144,10 @@ def load():
     L.qpd_get_info.restype = ctypes.c_int
     L.qpd_mc_frames.argtypes = [_P, ctypes.POINTER(QpdMcChannel), ctypes.c_uint64, _i64, _i64, _P, _P, _P]
     L.qpd_mc_frames.restype = ctypes.c_int
+    L.qpd_optls_quantizer.argtypes = [_P, _P, _i32, _i32, _i32, _P, _P, _P, _P]
+    L.qpd_optls_quantizer.restype = ctypes.c_int
+    L.qpd_lutgen_mindistortion.argtypes = [_i32, _i32, _P, _P, _i32, _i32, _P, _P, _P, _P]
+    L.qpd_lutgen_mindistortion.restype = ctypes.c_int
     if L.qpd_abi_version() != ABI_VERSION:
         raise ImportError("libqpd.so ABI version mismatch")
     _lib = L

@@ -41,6 +41,7 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
         "-I",
         SRC,
         os.path.join(SRC, "qpd_capi.hip"),
+        os.path.join(SRC, "qpd_lutgen.cpp"),
         "-o",
         LIB + ".tmp",
     ]

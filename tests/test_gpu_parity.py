@@ -333,3 +333,28 @@ def test_fast_engine_rejects_per_element_tables(qpd):
     fm, nt = _node_type(N, K)
     with pytest.raises(ValueError):
         qpd.from_packed("SCL-LUT", p, K, fm, L=4, engine="fast")
+
+
+@pytest.mark.parametrize("kind,L", [("SC-LUT", 1), ("SCL-LUT", 8), ("FastSC-LUT", 1), ("FastSCL-LUT", 4)])
+def test_gpu_with_designed_tables_matches_oracle(kind, L, qpd, oracle_mod):
+    """MinDistortion tables from lutgen.py and the drivers' channel quantizer
+    (the reference's whole pipeline), GPU vs oracle; BLER well below uncoded."""
+    from quantized_decoder_polar_codes_amd import codes as C
+    from quantized_decoder_polar_codes_amd import lutgen as LG
+    from quantized_decoder_polar_codes_amd import montecarlo as MC
+
+    N, K = 256, 128
+    d = LG.design(N, 16, 3.0)
+    _, mb, fm, mm = C.construct_pw(N, K)
+    nt = C.identify_nodes(N, mb).astype(np.int32)
+    sigma = MC.sigma_for(2.5, K / N)
+    _, _, edges, clut = LG.channel_quantizer(sigma, 128, 16)
+    rng = np.random.default_rng(11)
+    msg = rng.integers(0, 2, size=(400, K), dtype=np.uint8)
+    x = C.polar_encode(msg, mb, N)
+    llr = ((1.0 - 2.0 * x) + rng.normal(0, sigma, size=x.shape)) * 2 / sigma ** 2
+    sym = C.quantize_channel(llr, edges, clut, 16)
+    want = oracle_mod.decode_lut(kind, d.packed(), K, L, fm, sym, node_type=nt)
+    got = qpd.from_packed(kind, d.packed(), K, fm, L=L, node_type=nt).decode_batch(sym)
+    assert np.array_equal(got, want)
+    assert (got != msg).any(1).mean() < 0.5

@@ -23,7 +23,7 @@ buf = (ctypes.c_ulonglong * 64)()
 lib.qpd_debug_sel_stats(buf)
 cases = [("random 3..12", torch.from_numpy(np.random.default_rng(0).integers(3, 13, size=(F, N), dtype=np.int32)).cuda())]
 for eb in (1.0, 2.0, 3.0):
-    cases.append((f"AWGN {eb} dB", bench.synth_frames(N, K, F, eb, 1234, mb, torch.device("cuda", 0))[1]))
+    cases.append((f"AWGN {eb} dB", bench.workload(N, K, L, "SCL-LUT", F, eb, "minsum")[5]))
 for kind, sym in cases:
     d.decode_batch(sym)
     torch.cuda.synchronize()

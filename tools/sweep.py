@@ -18,15 +18,13 @@ N, K, L = (int(x) for x in sys.argv[2:5]) if len(sys.argv) > 4 else (1024, 512, 
 budgets = [int(x) for x in os.environ.get("SWEEP_BUDGETS", "8192,12288,16384,24576,32768").split(",")]
 frames_list = [int(x) for x in os.environ.get("SWEEP_FRAMES", "65536,262144").split(",")]
 waves_list = [int(x) for x in os.environ.get("SWEEP_WAVES", "0").split(",")]
-_, mb, fm, mm = C.construct_pw(N, K)
-nt = C.identify_nodes(N, mb).astype(np.int32)
-p = LU.minsum_uniform_luts(N)
-rng = np.random.default_rng(0)
-maxF = max(frames_list)
 import bench  # noqa: E402
 
-# the bench's workload: reference driver channel at Eb/N0 2 dB (data-dependent paths see realistic inputs)
-sym = bench.synth_frames(N, K, maxF, float(os.environ.get("SWEEP_EBN0", "2.0")), 1234, mb, torch.device("cuda", 0))[1]
+# the bench's workload (MinDistortion tables and channel quantizer, GPU frames at Eb/N0 2 dB)
+maxF = max(frames_list)
+_, packed, fm, nt, _, sym = bench.workload(N, K, L, kind, maxF, float(os.environ.get("SWEEP_EBN0", "2.0")),
+                                           os.environ.get("SWEEP_LUTS", "mindistortion"))
+p = packed
 ref = None
 for budget, F, mw in itertools.product(budgets, frames_list, waves_list):
     os.environ["QPD_LDS_BUDGET"] = str(budget)
