@@ -43,7 +43,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--kind", default="SCL-LUT", choices=["SC-LUT", "SCL-LUT", "FastSC-LUT", "FastSCL-LUT"])
+    ap.add_argument("--kind", default="SCL-LUT", choices=["SC-LUT", "SCL-LUT", "FastSC-LUT", "FastSCL-LUT", "CA-SCL-LUT",
+                                                          "CA-FastSCL-LUT"])
     ap.add_argument("--N", type=int, default=1024)
     ap.add_argument("--K", type=int, default=512)
     ap.add_argument("--L", type=int, default=8)
@@ -78,6 +79,8 @@ def workload(N, K, L, kind, frames, ebn0, luts="mindistortion", design_snr=3.0, 
     else:
         packed = LU.minsum_uniform_luts(N, v=16, delta=0.5)
         edges, clut = MC.uniform_channel_quantizer(16, 0.5)
+    if kind.startswith("CA-"):  # CRC-aided: A = K - 24 message bits + CRC-24 (the drivers' K = A + crc_n)
+        dec_kw.setdefault("A", K - 24)
     dec = Q.from_packed(kind, packed, K, fm, L=L, node_type=nt, device=device, **dec_kw)
     src = MC.GpuFrames(dec, edges, clut, 16, sigma, seed=1234)  # Philox keyed by global frame id
     msg, sym = src(frame0, frames)
@@ -92,7 +95,7 @@ import oracle
 from quantized_decoder_polar_codes_amd import lut as LU
 z = np.load(PATH, allow_pickle=False)
 R = oracle.reference_module()
-N, K, L, kind = int(z["N"]), int(z["K"]), int(z["L"]), str(z["kind"])
+N, K, L, kind, A = int(z["N"]), int(z["K"]), int(z["L"]), str(z["kind"]), int(z["A"])
 packed = LU.PackedLUT(N=N, v=int(z["v"]), lut_f=z["lut_f"], f_base=z["f_base"], f_step=0, lut_g=z["lut_g"],
                       g_base=z["g_base"], g_step=0, vcl=np.ascontiguousarray(z["vcl"]))
 fm, nt, sym = z["frozen"], z["node_type"], z["sym"]
@@ -102,10 +105,13 @@ if R is not None:
     dec = {"SC-LUT": lambda: R.SCLUTDecoder(N, K, fz, mm, fs, gs, vcl),
            "SCL-LUT": lambda: R.SCLLUTDecoder(N, K, L, fz, mm, fs, gs, vcl),
            "FastSC-LUT": lambda: R.FastSCLUTDecoder(N, K, fz, mm, nt.tolist(), fs, gs, vcl),
-           "FastSCL-LUT": lambda: R.FastSCLLUTDecoder(N, K, L, fz, mm, nt.tolist(), fs, gs, vcl)}[kind]()
+           "FastSCL-LUT": lambda: R.FastSCLLUTDecoder(N, K, L, fz, mm, nt.tolist(), fs, gs, vcl),
+           "CA-SCL-LUT": lambda: R.CASCLLUTDecoder(N, K, A, L, fz, mm, 24, list(oracle.CRC24_LOC), fs, gs, vcl),
+           "CA-FastSCL-LUT": lambda: R.CAFastSCLLUTDecoder(N, K, A, L, fz, mm, nt.tolist(), fs, gs, vcl)}[kind]()
     one = dec.decode
 else:
-    one = lambda s: oracle.decode_lut(kind, packed, K, L, fm, s[None], node_type=nt)[0]
+    one = (lambda s: oracle.decode_lut_ca(kind, packed, K, A, L, fm, s[None], node_type=nt)[0]) if kind.startswith("CA-") \
+        else (lambda s: oracle.decode_lut(kind, packed, K, L, fm, s[None], node_type=nt)[0])
 outs = []
 t0 = time.perf_counter()
 while time.perf_counter() - t0 < SECONDS and len(outs) < len(sym):
@@ -116,7 +122,7 @@ print(json.dumps({"frames": len(outs), "seconds": dt, "kind": "reference" if R i
 """
 
 
-def cpu_baseline(args, packed, fm, nt, sym, seconds, workers):
+def cpu_baseline(args, packed, fm, nt, sym, seconds, workers, A):
     """The reference decoder (oracle/_ref, compiled from /root/reference sources;
     the oracle restatement, kind "port", if that build is absent), one worker
     process per core, each decoding its own slice of the sample one frame per
@@ -129,7 +135,7 @@ def cpu_baseline(args, packed, fm, nt, sym, seconds, workers):
     procs = []
     for w in range(workers):
         path = os.path.join(tmp, f"w{w}.npz")
-        np.savez(path, N=args.N, K=args.K, L=args.L, kind=args.kind, v=packed.v, lut_f=packed.lut_f,
+        np.savez(path, N=args.N, K=args.K, A=A, L=args.L, kind=args.kind, v=packed.v, lut_f=packed.lut_f,
                  f_base=packed.f_base, lut_g=packed.lut_g, g_base=packed.g_base, vcl=packed.vcl, frozen=fm,
                  node_type=nt, sym=sym[w * per:(w + 1) * per])
         code = _WORKER.replace("ROOT", repr(ROOT)).replace("PATH", repr(path)).replace("SECONDS", repr(seconds))
@@ -247,7 +253,7 @@ def main():
                        "engine": {1: "generic", 2: "fast"}[info["engine"]], "lds_bytes_per_wave": info["lds_bytes_per_wave"],
                        "lds_from_depth": info["lds_from_depth"], "waves": min(info["max_waves"],
                        -(-args.frames // info["frames_per_wave"]))},
-            "ber": bit_errs / max(1, frames_all * K),
+            "ber": bit_errs / max(1, frames_all * dec.out_bits),
             "bler": blk_errs / max(1, frames_all),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -259,7 +265,8 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             workers = args.cpu_workers or min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
             sample = d_sym[: 1 << 15].cpu().numpy()
-            cb, parts = cpu_baseline(args, packed, fm, nt, sample, args.cpu_baseline_seconds, max(1, workers))
+            cb, parts = cpu_baseline(args, packed, fm, nt, sample, args.cpu_baseline_seconds, max(1, workers),
+                                     dec.out_bits)
             res["cpu_baseline"] = cb
             gpu_out = out.cpu().numpy()
             ok = all(np.array_equal(gpu_out[o:o + len(r)], r) for o, r in parts)
