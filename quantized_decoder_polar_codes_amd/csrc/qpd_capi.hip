@@ -112,7 +112,7 @@ struct qpd_decoder {
     bool l8 = false;  // fast engine: list decoder with L = 8 (select_survivors8)
     DevPlan plan{};
     qpd::FastPlan fplan{};
-    DeviceBuf f_tab, g_tab, fscratch, mops;
+    DeviceBuf f_tab, g_tab, fscratch, mops, r1_rank;
     int num_mops = 0;
     std::vector<Op> ops_host;
     DeviceBuf lut_f, f_base, lut_g, g_base, vcl, ops, info_pos, scratch, err;
@@ -203,11 +203,34 @@ int validate(const qpd_config *c, int *n_out) {
 struct FastLayout {
     int D = 0;
     int S[qpd::kMaxDepth + 1] = {}, U[qpd::kMaxDepth + 1] = {}, R[qpd::kMaxDepth + 1] = {};
+    // LDS rows are grouped by depth (R, S, U of depth D, then of D+1, ...) and
+    // followed by the set's selection scratch, so that the rows of all depths
+    // > d form one contiguous tail: free scratch while a special node at
+    // depth d (which replaces its whole subtree) runs.
+    int lds_base[qpd::kMaxDepth + 2] = {};  // first LDS row of depth dd (dd >= D)
+    int lds_end = 0;                        // rows incl. the selection scratch
     bool lds(int dd) const { return dd >= D; }
 };
 
+// R1 argsort keys of the fast engine (FastSCL, node size <= 32): for element j
+// and symbol s of the node, (rank of |vcl[d-1][pos_j][s]| among all the node's
+// magnitudes) << 1 | (vcl < 0).  Equal magnitudes get equal ranks, so
+// comparing ranks is comparing the doubles (H1 tie behaviour intact).
+void r1_rank_table(std::vector<uint16_t> &tab, const double *vcl, int N, int v, int d, int node) {
+    const int temp = N >> d;
+    const double *q = vcl + ((size_t)(d - 1) * N + (size_t)temp * node) * v;
+    std::vector<double> mags;
+    for (int i = 0; i < temp * v; ++i) mags.push_back(std::fabs(q[i]));
+    std::sort(mags.begin(), mags.end());
+    mags.erase(std::unique(mags.begin(), mags.end()), mags.end());
+    for (int i = 0; i < temp * v; ++i) {
+        const int r = (int)(std::lower_bound(mags.begin(), mags.end(), std::fabs(q[i])) - mags.begin());
+        tab.push_back((uint16_t)((r << 1) | (q[i] < 0 ? 1 : 0)));
+    }
+}
+
 void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N, int n, int v, const int32_t *frozen,
-              const int32_t *node_type, int d, int node) {
+              const int32_t *node_type, const double *vcl, std::vector<uint16_t> &r1tab, int d, int node) {
     using namespace qpd;
     const int posi = (1 << d) + node - 1;
     auto base = [&](int type) {
@@ -237,6 +260,16 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
         MOp m = base(OP_R0 + t);
         m.cnt = N >> d;
         m.vrow = (d - 1) * N + (N >> d) * node;
+        if (kind == QPD_FASTSCL_LUT && OP_R0 + t == OP_R1 && m.cnt <= 32) {
+            m.tab = (int)r1tab.size();  // rank-key table of this node
+            r1_rank_table(r1tab, vcl, N, v, d, node);
+            // > 16 elements: std::sort's introsort runs on 16-bit entries in the
+            // free LDS tail (rows of depths > d + the selection scratch)
+            if (m.cnt > qpd::stl::kThreshold && Ly.lds(d + 1) && Ly.lds_end - Ly.lds_base[d + 1] >= m.cnt / 2) {
+                m.flags |= MF_R1_LDS;
+                m.u_row = Ly.lds_base[d + 1];
+            }
+        }
         finish_node(m);
         out.push_back(m);
         return;
@@ -272,7 +305,7 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
                 m.tab = posi * 32;
             }
             out.push_back(m);
-            fast_ops(out, Ly, kind, N, n, v, frozen, node_type, d + 1, 2 * node + side);
+            fast_ops(out, Ly, kind, N, n, v, frozen, node_type, vcl, r1tab, d + 1, 2 * node + side);
         }
     } else {
         for (int side = 0; side < 2; ++side) {
@@ -393,21 +426,22 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     while (Ly.D <= n && NS * (qpd::kSelInts * 4 + lds_rows(Ly.D) * 256) > budget) ++Ly.D;
     F.lds_from = Ly.D;
     int rl = 0, rg = 0;
-    for (int dd = 1; dd <= n - 1; ++dd) {
+    for (int dd = 0; dd <= n; ++dd) {  // grouped by depth (see FastLayout)
         int &r = Ly.lds(dd) ? rl : rg;
-        Ly.S[dd] = r;
-        r += srows(dd);
-    }
-    for (int dd = 1; dd <= n; ++dd) {
-        int &r = Ly.lds(dd) ? rl : rg;
-        Ly.U[dd] = r;
-        r += brows(dd);
-    }
-    for (int dd = 0; dd <= n; ++dd) {
-        int &r = Ly.lds(dd) ? rl : rg;
+        if (Ly.lds(dd)) Ly.lds_base[dd] = r;
         Ly.R[dd] = r;
         r += brows(dd);
+        if (dd >= 1 && dd <= n - 1) {
+            Ly.S[dd] = r;
+            r += srows(dd);
+        }
+        if (dd >= 1) {
+            Ly.U[dd] = r;
+            r += brows(dd);
+        }
     }
+    Ly.lds_base[n + 1] = rl;
+    Ly.lds_end = rl + qpd::kSelInts / 64;
     F.R0_row = Ly.R[0];
     F.R0_lds = Ly.lds(0);
     F.H_row = F.K_row = F.I_row = rg;
@@ -423,8 +457,15 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     F.glb_rows = std::max(rg, 1);
     d->lds_bytes = NS * (qpd::kSelInts * 4 + rl * 256);
     std::vector<qpd::MOp> mops;
+    std::vector<uint16_t> r1tab;
     fast_ops(mops, Ly, c->kind, N, n, v, c->frozen_bits,
-             (c->kind == QPD_FASTSC_LUT || c->kind == QPD_FASTSCL_LUT) ? c->node_type : nullptr, 0, 0);
+             (c->kind == QPD_FASTSC_LUT || c->kind == QPD_FASTSCL_LUT) ? c->node_type : nullptr, c->vcl, r1tab, 0, 0);
+    if (r1tab.empty()) r1tab.push_back(0);
+    {
+        int rc = upload(d->r1_rank, r1tab.data(), r1tab.size());
+        if (rc) return rc;
+    }
+    F.r1_rank = (const uint16_t *)d->r1_rank.p;
     place_syncs(mops, c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT);
     F.nops = (int)mops.size();
     d->num_mops = F.nops;

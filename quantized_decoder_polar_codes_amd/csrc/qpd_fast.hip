@@ -40,6 +40,7 @@ enum MopFlag : int32_t {
     MF_SYNC = 16,     // drain the global slab before this op (see place_syncs)
     MF_R_LDS = 32,    // R rows read by the op (COMB) in LDS
     MF_CHAN = 64,     // S[d] is the channel input (d == 0)
+    MF_R1_LDS = 128,  // R1 (> 16 elements): argsort in the free LDS tail starting at row u_row
 };
 
 struct MOp {
@@ -52,7 +53,7 @@ struct MOp {
     int32_t sh_src;   // 4*d: ps field of S[d]
     int32_t sh_u;     // G/COMB: 4*(d+1); LEAF_R: 4*n
     int32_t sh_dst;   // F/G: 4*(d+1) (ps); COMB/special/BOT3 left child: 4*d (pu); LEAF_L: 4*n (pu)
-    int32_t tab;      // F/LEAF_L: posi*32; G/LEAF_R: posi*64; BOT3: posi of the subtree root
+    int32_t tab;      // F/LEAF_L: posi*32; G/LEAF_R: posi*64; BOT3: posi of the subtree root; R1: r1_rank offset
     int32_t vrow;     // LEAF: ((n-1)*N + k)*v; special: (d-1)*N + temp*node; BOT3: ((n-1)*N + 8*node)*v
     int32_t pad0, pad1;
 };
@@ -72,6 +73,7 @@ struct FastPlan {
     const double *vcl;            // [rows][N][v]
     const MOp *ops;
     const int32_t *info_pos;
+    const uint16_t *r1_rank;      // FastSCL R1 (<= 32 elements): [temp][v] rank << 1 | sign, per node at op.tab
     uint32_t *scratch;            // [waves][glb_rows][64]
     int32_t *err;
 };
@@ -375,7 +377,7 @@ __device__ __forceinline__ uint32_t leaf_fork(Path &st, double dm, int gl, int g
 // One leaf decision for every set.  `frozen` is wave-uniform.
 template <bool kList, bool L8, int NS, int NX>
 __device__ __forceinline__ void leaf_decide(Path (&st)[NS], const double (&dm)[NS], bool frozen, int gl, int gbase,
-                                            int L, int lane, int *sel, uint32_t (&extra)[NS][NX],
+                                            int L, int lane, int *sel, int sstride, uint32_t (&extra)[NS][NX],
                                             uint32_t (&dec)[NS]) {
     if (!kList) {
 #pragma unroll
@@ -391,7 +393,7 @@ __device__ __forceinline__ void leaf_decide(Path (&st)[NS], const double (&dm)[N
         return;
     }
 #pragma unroll
-    for (int s = 0; s < NS; ++s) dec[s] = leaf_fork<L8>(st[s], dm[s], gl, gbase, L, lane, sel + kSelInts * s, extra[s]);
+    for (int s = 0; s < NS; ++s) dec[s] = leaf_fork<L8>(st[s], dm[s], gl, gbase, L, lane, sel + sstride * s, extra[s]);
 }
 
 // ---------------------------------------------------------------------------
@@ -412,7 +414,7 @@ __device__ __forceinline__ uint32_t g_pair(uint32_t T, uint32_t c2, uint32_t w2)
 
 template <bool kList, bool L8, int NS>
 __device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], uint32_t Tf, int fo, uint32_t Tg,
-                                         double V, int vo, int fr, int gl, int gbase, int L, int lane, int *sel,
+                                         double V, int vo, int fr, int gl, int gbase, int L, int lane, int *sel, int sstride,
                                          uint32_t (&c)[NS]) {
     double dm[NS];
     uint32_t bl[NS], br[NS];
@@ -422,14 +424,14 @@ __device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], u
         dm[s] = 0;
         if (kList || !(fr & 1)) dm[s] = shfld(V, vo + (int)lut4(Tf, ((a << 4) | b) + fo));
     }
-    leaf_decide<kList, L8>(st, dm, fr & 1, gl, gbase, L, lane, sel, x, bl);
+    leaf_decide<kList, L8>(st, dm, fr & 1, gl, gbase, L, lane, sel, sstride, x, bl);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         x[s][1] = (x[s][1] & ~(1u << 24)) | (bl[s] << 24);
         const uint32_t a = (x[s][1] >> 16) & 15u, b = (x[s][1] >> 20) & 15u;
         if (kList || !(fr & 2)) dm[s] = shfld(V, vo + 16 + (int)lut4(Tg, (bl[s] << 8) | (a << 4) | b));
     }
-    leaf_decide<kList, L8>(st, dm, fr & 2, gl, gbase, L, lane, sel, x, br);
+    leaf_decide<kList, L8>(st, dm, fr & 2, gl, gbase, L, lane, sel, sstride, x, br);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const uint32_t bl2 = (x[s][1] >> 24) & 1u;
@@ -440,7 +442,7 @@ __device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], u
 template <bool kList, bool L8, int NS>
 __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], const MOp &op,
                                         const int32_t *const (&y)[NS], Path (&st)[NS], uint32_t Tf0, int gl, int gbase,
-                                        int L, int *sel, int lane) {
+                                        int L, int *sel, int sstride, int lane) {
     const int p0 = op.tab * QPD_EXP_TABMUL;
     const int fr = op.cnt;
     const uint32_t *ft = P.f_tab, *gt = P.g_tab;
@@ -469,13 +471,13 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
         const uint32_t w2 = lut_vec<4>(Tf0, x[s][0], x[s][0] >> 16, 0u);
         x[s][1] = w2 | (f_pair(Tf12, 0u, w2) << 16);
     }
-    bot_pair<kList, L8>(st, x, Tf34, 0, Tg3, Vlo, 0, fr, gl, gbase, L, lane, sel, c);  // leaves 0, 1
+    bot_pair<kList, L8>(st, x, Tf34, 0, Tg3, Vlo, 0, fr, gl, gbase, L, lane, sel, sstride, c);  // leaves 0, 1
 #pragma unroll
     for (int s = 0; s < NS; ++s) {  // q1: W1 = g(W2, c2)
         x[s][1] = (x[s][1] & ~(3u << 25)) | (c[s] << 25);
         x[s][1] = (x[s][1] & ~(0xffu << 16)) | (g_pair(Tg1, c[s], x[s][1] & 0xffffu) << 16);
     }
-    bot_pair<kList, L8>(st, x, Tf34, 256, Tg4, Vlo, 32, fr >> 2, gl, gbase, L, lane, sel, c);  // leaves 2, 3
+    bot_pair<kList, L8>(st, x, Tf34, 256, Tg4, Vlo, 32, fr >> 2, gl, gbase, L, lane, sel, sstride, c);  // leaves 2, 3
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const uint32_t c2 = (x[s][1] >> 25) & 3u;
@@ -484,13 +486,13 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
         const uint32_t w2 = lut_vec<4>(Tg0, x[s][0], x[s][0] >> 16, c3);
         x[s][1] = w2 | (f_pair(Tf12, 3u, w2) << 16) | (c3 << 27);
     }
-    bot_pair<kList, L8>(st, x, Tf56, 0, Tg5, Vhi, 0, fr >> 4, gl, gbase, L, lane, sel, c);  // leaves 4, 5
+    bot_pair<kList, L8>(st, x, Tf56, 0, Tg5, Vhi, 0, fr >> 4, gl, gbase, L, lane, sel, sstride, c);  // leaves 4, 5
 #pragma unroll
     for (int s = 0; s < NS; ++s) {  // q2: W1 = g(W2, c2)
         x[s][1] = (x[s][1] & ~(3u << 25)) | (c[s] << 25);
         x[s][1] = (x[s][1] & ~(0xffu << 16)) | (g_pair(Tg2, c[s], x[s][1] & 0xffffu) << 16);
     }
-    bot_pair<kList, L8>(st, x, Tf56, 256, Tg6, Vhi, 32, fr >> 6, gl, gbase, L, lane, sel, c);  // leaves 6, 7
+    bot_pair<kList, L8>(st, x, Tf56, 256, Tg6, Vhi, 32, fr >> 6, gl, gbase, L, lane, sel, sstride, c);  // leaves 6, 7
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const uint32_t c2 = (x[s][1] >> 25) & 3u;
@@ -501,6 +503,324 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
     }
 }
 
+// ---------------------------------------------------------------------------
+// Special nodes of the Fast decoders (FastSCLUT.cpp:46-107,
+// FastSCLLUTDecoder.cpp:82-213).  The node's symbols are read a word (8
+// symbols) at a time and their quanta vcl[d-1][pos][sym] (H3) fetched 8 at a
+// time, so a node costs one memory round trip per 8 elements; sums still run
+// in the reference's sequential element order (H5).
+// ---------------------------------------------------------------------------
+
+// LDS view of the R1 argsort array: 16-bit entries (rank << 5 | element),
+// entry p of this lane at row base + p/2, half p%2 of the lane's dword.
+struct LdsSeq16 {
+    uint16_t *lane0;  // &row[base][lane] as 16-bit
+    __device__ __forceinline__ int get(int p) const { return lane0[(p >> 1) * 128 + (p & 1)]; }
+    __device__ __forceinline__ void set(int p, int e) const { lane0[(p >> 1) * 128 + (p & 1)] = (uint16_t)e; }
+    __device__ __forceinline__ bool less(int a, int b) const { return (a >> 5) < (b >> 5); }  // keys only, as std::sort
+};
+
+// Survivor layers of an R1 node (FastSCLLUTDecoder.cpp:118-166) after its
+// argsort: ord[q] / ms[q] = element and magnitude of the q-th smallest |llr|,
+// hw = hard decisions (l < 0).  Each of the m layers forks on flipping the
+// next element; ord/ms/flip follow the surviving lineage, the flip position
+// is the lane's own pre-permutation ord (H2).  Returns the node's bits.
+template <bool L8>
+__device__ __forceinline__ uint32_t r1_layers(Path &st, int *sel, int gl, int gbase, int lane, int L, int m, int (&ord)[kMaxM],
+                                              double (&ms)[kMaxM], uint32_t hw, int temp) {
+    int flip[kMaxM];
+#pragma unroll
+    for (int q = 0; q < kMaxM; ++q) flip[q] = -1;
+    int origin = gl;
+#pragma unroll
+    for (int layer = 0; layer < kMaxM; ++layer) {
+        if (layer < m) {
+            const double kf = st.pm + ms[layer];
+            const Sel sl = L8 ? select_survivors8(st.pm, kf, gl, gbase, lane, sel)
+                              : select_survivors(st.pm, kf, gl, gbase, L, sel);
+            const int p = gbase + sl.parent;
+            const int pos_old = ord[layer];  // H2
+            st.pm = pick(sl.upper, shfld(kf, p), shfld(st.pm, p));
+            st.ps = shfl64(st.ps, p);
+            st.pu = shfl64(st.pu, p);
+            origin = __shfl(origin, p);
+#pragma unroll
+            for (int q = 0; q < kMaxM; ++q) {
+                ord[q] = __shfl(ord[q], p);
+                ms[q] = shfld(ms[q], p);
+                if (q < layer) flip[q] = __shfl(flip[q], p);
+            }
+            flip[layer] = sl.upper ? pos_old : -1;
+        }
+    }
+    uint32_t word = (uint32_t)__shfl((int)hw, gbase + origin);
+#pragma unroll
+    for (int q = 0; q < kMaxM; ++q)
+        if (q < m && flip[q] >= 0) word ^= 1u << (flip[q] & 31);
+    return temp < 32 ? word & ((1u << temp) - 1u) : word;
+}
+
+// R1 node of FastSCL-LUT with at most 32 elements (FastSCLLUTDecoder.cpp:99-166).
+// Argsort keys are the host-built ranks of |llr| (r1_rank: equal magnitudes,
+// equal ranks), so everything stays in registers / LDS:
+//   <= 16 elements: libstdc++ sorts by insertion (stable), i.e. by
+//     (rank, element): the m smallest 32-bit entries rank << 5 | element;
+//   17..32 elements: the exact introsort replay (stl::sort_small) on 16-bit
+//     entries in the free LDS tail (MF_R1_LDS; rows of depths > d).
+template <bool L8>
+__device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const MOp &op, Path &st, int *sel, int gl,
+                                         int gbase, int L, int lane, int temp) {
+    const int src = gbase + pfield(st.ps, op.sh_src);
+    const bool sl = op.flags & MF_SRC_LDS;
+    const int v = P.v;
+    const int m = (L - 1) < temp ? (L - 1) : temp;
+    const uint16_t *rk = P.r1_rank + op.tab;
+    const double *vq = P.vcl + (size_t)op.vrow * v;
+    uint32_t W[4], hw = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) W[w] = (8 * w < temp) ? M.ld(sl, op.src_row + w, src) : 0u;
+    int ord[kMaxM];
+#pragma unroll
+    for (int q = 0; q < kMaxM; ++q) ord[q] = 0;
+    if (temp <= stl::kThreshold) {
+        uint32_t ent[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            ent[j] = 0xffffffffu;
+            if (j < temp) {
+                const uint32_t e = rk[j * v + ((W[j >> 3] >> (4 * (j & 7))) & 15u)];
+                hw |= (e & 1u) << j;
+                ent[j] = ((e >> 1) << 5) | (uint32_t)j;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kMaxM; ++q) {
+            if (q < m) {
+                uint32_t mn = ent[0];
+#pragma unroll
+                for (int j = 1; j < 16; ++j) mn = ent[j] < mn ? ent[j] : mn;
+                ord[q] = (int)(mn & 31u);
+#pragma unroll
+                for (int j = 0; j < 16; ++j) ent[j] = ent[j] == mn ? 0xffffffffu : ent[j];
+            }
+        }
+    } else {
+        const LdsSeq16 seq{(uint16_t *)(M.lds + op.u_row * 64 + lane)};
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            if (j < temp) {
+                const uint32_t e = rk[j * v + ((W[j >> 3] >> (4 * (j & 7))) & 15u)];
+                hw |= (e & 1u) << j;
+                seq.set(j, (int)(((e >> 1) << 5) | (uint32_t)j));
+            }
+        }
+        stl::sort_small(seq, 0, temp);
+#pragma unroll
+        for (int q = 0; q < kMaxM; ++q)
+            if (q < m) ord[q] = seq.get(q) & 31;
+    }
+    double ms[kMaxM];
+#pragma unroll
+    for (int q = 0; q < kMaxM; ++q) {
+        ms[q] = 0;
+        if (q < m) {
+            const int k = ord[q] >> 3;
+            const uint32_t w = k == 0 ? W[0] : k == 1 ? W[1] : k == 2 ? W[2] : W[3];
+            ms[q] = fabs(vq[(size_t)ord[q] * v + ((w >> (4 * (ord[q] & 7))) & 15u)]);
+        }
+    }
+    const uint32_t word = r1_layers<L8>(st, sel, gl, gbase, lane, L, m, ord, ms, hw, temp);
+    M.st(op.flags & MF_DST_LDS, op.dst_row, lane, word);
+}
+
+// R1 nodes above 32 elements (N >= 2048 codes) or without LDS room: the
+// argsort arrays live in the wave's global slab (H / K / I rows).
+__device__ __forceinline__ void r1_large(const FastPlan &P, const Mem &M, const MOp &op, Path &st, int *sel, int gl,
+                                      int gbase, int L, int lane, int temp) {
+    const int src = gbase + pfield(st.ps, op.sh_src);
+    const bool sl = op.flags & MF_SRC_LDS, dl = op.flags & MF_DST_LDS;
+    const int nwo = (temp + 31) >> 5;
+    const double *vq = P.vcl + (size_t)op.vrow * P.v;
+    auto llr = [&](int j) -> double {
+        const uint32_t w = M.ld(sl, op.src_row + (j >> 3), src);
+        return vq[(size_t)j * P.v + ((w >> ((j & 7) << 2)) & 15u)];
+    };
+    const int m = (L - 1) < temp ? (L - 1) : temp;
+    uint32_t *g = M.gp;
+    for (int w = 0; w < nwo; ++w) {
+        uint32_t word = 0;
+        for (int i = 0; i < 32 && 32 * w + i < temp; ++i) {
+            const int j = 32 * w + i;
+            const double l = llr(j);
+            word |= (uint32_t)(l < 0) << i;
+            ((double *)(g + (size_t)(P.K_row + 2 * j) * 64))[lane] = fabs(l);
+        }
+        g[(size_t)(P.H_row + w) * 64 + lane] = word;
+    }
+    int ord[kMaxM];
+    double ms[kMaxM];
+    int flip[kMaxM];
+    for (int q = 0; q < kMaxM; ++q) {
+        ord[q] = 0;
+        ms[q] = 0;
+        flip[q] = -1;
+    }
+    FastSortSeq seq{g, P.I_row, P.K_row, lane};
+    for (int p = 0; p < temp; ++p) seq.set(p, p);
+    stl::sort(seq, 0, temp);
+    for (int q = 0; q < kMaxM; ++q) {
+        if (q < m) {
+            ord[q] = seq.get(q);
+            ms[q] = seq.key(ord[q]);
+        }
+    }
+    wave_sync();  // H rows visible to the whole wave
+    int origin = gl;
+    for (int layer = 0; layer < kMaxM; ++layer) {
+        if (layer < m) {
+            const double kf = st.pm + ms[layer];
+            const Sel sx = select_survivors(st.pm, kf, gl, gbase, L, sel);
+            const int p = gbase + sx.parent;
+            const int pos_old = ord[layer];  // H2
+            st.pm = pick(sx.upper, shfld(kf, p), shfld(st.pm, p));
+            st.ps = shfl64(st.ps, p);
+            st.pu = shfl64(st.pu, p);
+            origin = __shfl(origin, p);
+            for (int q = 0; q < kMaxM; ++q) {
+                ord[q] = __shfl(ord[q], p);
+                ms[q] = shfld(ms[q], p);
+                if (q < layer) flip[q] = __shfl(flip[q], p);
+            }
+            flip[layer] = sx.upper ? pos_old : -1;
+        }
+    }
+    for (int w = 0; w < nwo; ++w) {
+        uint32_t word = g[(size_t)(P.H_row + w) * 64 + gbase + origin];
+        for (int q = 0; q < kMaxM; ++q)
+            if (q < m && flip[q] >= 0 && (flip[q] >> 5) == w) word ^= 1u << (flip[q] & 31);
+        if (temp < 32) word &= (1u << temp) - 1u;
+        M.st(dl, op.dst_row + w, lane, word);
+    }
+}
+
+template <bool kList, bool L8>
+__device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, const MOp &op, Path &st, int *sel, int gl,
+                                           int gbase, int L, int lane) {
+    const int fl = op.flags;
+    const int temp = op.cnt;
+    const int src = gbase + pfield(st.ps, op.sh_src);
+    const bool dl = fl & MF_DST_LDS, sl = fl & MF_SRC_LDS;
+    const int nwo = (temp + 31) >> 5;
+    const int v = P.v;
+    const double *vq = P.vcl + (size_t)op.vrow * v;  // row d-1, position temp*node
+    // elements [8w, 8w + 8) of the node: quanta of its symbols
+    auto llr8 = [&](int w, double (&l)[8], uint32_t &word) {
+        word = M.ld(sl, op.src_row + w, src);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            l[i] = (8 * w + i < temp) ? vq[(size_t)(8 * w + i) * v + ((word >> (4 * i)) & 15u)] : 0.0;
+    };
+    const int n8 = (temp + 7) >> 3;
+    if (op.type == OP_R0) {
+        if (kList) {
+            for (int w = 0; w < n8; ++w) {
+                double l[8];
+                uint32_t word;
+                llr8(w, l, word);
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if (8 * w + i < temp) st.pm += (double)(float)(l[i] < 0) * fabs(l[i]);  // H5
+            }
+        }
+        for (int w = 0; w < nwo; ++w) M.st(dl, op.dst_row + w, lane, 0u);
+    } else if (op.type == OP_REP) {
+        uint32_t fill = 0;
+        if (!kList) {
+            double S = 0;
+            for (int w = 0; w < n8; ++w) {
+                double l[8];
+                uint32_t word;
+                llr8(w, l, word);
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if (8 * w + i < temp) S += l[i];
+            }
+            fill = S <= 0 ? 0xffffffffu : 0u;  // H4
+        } else {
+            double kk = st.pm, kf = st.pm;
+            for (int w = 0; w < n8; ++w) {
+                double l[8];
+                uint32_t word;
+                llr8(w, l, word);
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if (8 * w + i < temp) {
+                        kk += (double)(l[i] < 0) * fabs(l[i]);
+                        kf += (double)(l[i] >= 0) * fabs(l[i]);
+                    }
+            }
+            const Sel sx = L8 ? select_survivors8(kk, kf, gl, gbase, lane, sel) : select_survivors(kk, kf, gl, gbase, L, sel);
+            const int p = gbase + sx.parent;
+            st.pm = pick(sx.upper, shfld(kf, p), shfld(kk, p));
+            st.ps = shfl64(st.ps, p);
+            st.pu = shfl64(st.pu, p);
+            fill = sx.upper ? 0xffffffffu : 0u;
+        }
+        const uint32_t m = temp < 32 ? ((1u << temp) - 1u) : 0xffffffffu;
+        for (int w = 0; w < nwo; ++w) M.st(dl, op.dst_row + w, lane, fill & m);
+    } else if (op.type == OP_SPC) {  // FastSC only
+        uint32_t parity = 0, word = 0;
+        double best = 0;
+        int bi = 0;
+        for (int w = 0; w < n8; ++w) {
+            double l[8];
+            uint32_t sw;
+            llr8(w, l, sw);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int j = 8 * w + i;
+                if (j < temp) {
+                    const uint32_t h = l[i] <= 0;
+                    word |= h << (j & 31);
+                    parity ^= h;
+                    const double a = fabs(l[i]);
+                    if (j == 0 || a < best) {  // first minimum (H6)
+                        best = a;
+                        bi = j;
+                    }
+                }
+            }
+            if ((w & 3) == 3 || w == n8 - 1) {
+                M.st(dl, op.dst_row + (w >> 2), lane, word);
+                word = 0;
+            }
+        }
+        if (parity) {
+            const int row = op.dst_row + (bi >> 5);
+            M.st(dl, row, lane, M.ld(dl, row, lane) ^ (1u << (bi & 31)));
+        }
+    } else if (!kList) {  // OP_R1, FastSC: `<= 0`
+        uint32_t word = 0;
+        for (int w = 0; w < n8; ++w) {
+            double l[8];
+            uint32_t sw;
+            llr8(w, l, sw);
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (8 * w + i < temp) word |= (uint32_t)(l[i] <= 0) << ((8 * w + i) & 31);
+            if ((w & 3) == 3 || w == n8 - 1) {
+                M.st(dl, op.dst_row + (w >> 2), lane, word);
+                word = 0;
+            }
+        }
+    } else if (temp <= stl::kThreshold || (fl & MF_R1_LDS)) {
+        r1_small<L8>(P, M, op, st, sel, gl, gbase, L, lane, temp);
+    } else {
+        r1_large(P, M, op, st, sel, gl, gbase, L, lane, temp);
+    }
+    if (!(fl & MF_TO_R)) st.pu = pset(st.pu, op.sh_dst, gl);
+}
+
 #ifdef QPD_STAMPS
 // Diagnostic build only: wave cycles per op class (lane k of each wave
 // accumulates class k; flushed once per wave).  Class = 2*type + (op syncs).
@@ -508,9 +828,13 @@ __device__ unsigned long long qpd_stamp_acc[64];
 #endif
 
 // Waves per SIMD the register allocation targets: 6 (80 VGPRs) for one
-// frame set, 4 (128 VGPRs) for two -- the measured optima on MI355X.
+// frame set, 4 (128 VGPRs) for two, 5 (96 VGPRs) for FastSCL's one set (its
+// R1 argsort state spills the main loop at 80) -- the measured optima on MI355X.
 #ifndef QPD_WPE1
 #define QPD_WPE1 6
+#endif
+#ifndef QPD_WPE_FSCL
+#define QPD_WPE_FSCL 5
 #endif
 #ifndef QPD_WPE2
 #define QPD_WPE2 4
@@ -522,16 +846,18 @@ template <int KIND, int NS, bool L8>
 // `ops` is its own __restrict__ argument (= P.ops) so that the compiler can
 // prove the op records are never written and fetch them with scalar loads
 // instead of vector loads + readfirstlane, which drain vmcnt at every op.
-__global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : QPD_WPE1) void lut_fast_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
+__global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QPD_WPE_FSCL : QPD_WPE1) void lut_fast_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
                                                                uint8_t *__restrict__ out,
                                                                const MOp *__restrict__ ops) {
     constexpr bool kList = (KIND == K_SCL_LUT || KIND == K_FASTSCL_LUT);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
-    int *const sel_all = (int *)lds_dyn;
+    // per set: [lds_rows rows][selection scratch] (rows grouped by depth, see FastLayout)
+    const int sstride = P.lds_rows * 64 + kSelInts;
+    int *const sel_all = (int *)(lds_dyn + P.lds_rows * 64);
     Mem Mv[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-        Mv[s].lds = lds_dyn + NS * kSelInts + s * P.lds_rows * 64;
+        Mv[s].lds = lds_dyn + s * sstride;
         Mv[s].gp = P.scratch + ((size_t)blockIdx.x * NS + s) * P.glb_rows * 64;
         Mv[s].rs = __builtin_amdgcn_make_buffer_rsrc(Mv[s].gp, 0, P.glb_rows * 256 * QPD_EXP_SLABMUL, 0x00020000);
     }
@@ -591,7 +917,7 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : QPD_WPE1) void lut_fast_ke
             const int fl = op.flags;
             switch (op.type) {
                 case OP_BOT3:
-                    bot3_op<kList, L8>(P, Mv, op, yv, stv, cur.T, gl, gbase, L, sel_all, lane);
+                    bot3_op<kList, L8>(P, Mv, op, yv, stv, cur.T, gl, gbase, L, sel_all, sstride, lane);
                     break;
                 case OP_F:
                 case OP_G: {
@@ -627,7 +953,7 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : QPD_WPE1) void lut_fast_ke
                             dm[s] = shfld(cur.V, (int)lut4(cur.T, idx));  // vcl[n-1][k][s] (H3)
                         }
                     }
-                    leaf_decide<kList, L8>(stv, dm, frozen, gl, gbase, L, lane, sel_all, none, dec);
+                    leaf_decide<kList, L8>(stv, dm, frozen, gl, gbase, L, lane, sel_all, sstride, none, dec);
 #pragma unroll
                     for (int s = 0; s < NS; ++s) {
                         Mv[s].st(fl & MF_DST_LDS, op.dst_row, lane, dec[s]);
@@ -671,163 +997,8 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : QPD_WPE1) void lut_fast_ke
                   for (int s = 0; s < NS; ++s) {
                     Path &st = stv[s];
                     const Mem &M = Mv[s];
-                    int *const sel = sel_all + kSelInts * s;
-                        const int temp = op.cnt;
-                        const int src = gbase + pfield(st.ps, op.sh_src);
-                        const bool dl = fl & MF_DST_LDS;
-                        const int nwo = (temp + 31) >> 5;
-                        const double *vq = P.vcl + (size_t)op.vrow * P.v;  // row d-1, position temp*node
-                        auto sym = [&](int j) -> int {
-                            const uint32_t w = M.ld(fl & MF_SRC_LDS, op.src_row + (j >> 3), src);
-                            return (int)((w >> ((j & 7) << 2)) & 15u);
-                        };
-                        auto llr = [&](int j) -> double { return vq[(size_t)j * P.v + sym(j)]; };
-                        if (op.type == OP_R0) {
-                            if (kList) {
-                                for (int j = 0; j < temp; ++j) {
-                                    const double l = llr(j);
-                                    st.pm += (double)(float)(l < 0) * fabs(l);
-                                }
-                            }
-                            for (int w = 0; w < nwo; ++w) M.st(dl, op.dst_row + w, lane, 0u);
-                        } else if (op.type == OP_REP) {
-                            uint32_t fill = 0;
-                            if (!kList) {
-                                double S = 0;
-                                for (int j = 0; j < temp; ++j) S += llr(j);
-                                fill = S <= 0 ? 0xffffffffu : 0u;
-                            } else {
-                                double kk = st.pm, kf = st.pm;
-                                for (int j = 0; j < temp; ++j) {
-                                    const double l = llr(j);
-                                    kk += (double)(l < 0) * fabs(l);
-                                    kf += (double)(l >= 0) * fabs(l);
-                                }
-                                const Sel sl = select_survivors(kk, kf, gl, gbase, L, sel);
-                                const int p = gbase + sl.parent;
-                                st.pm = pick(sl.upper, shfld(kf, p), shfld(kk, p));
-                                st.ps = shfl64(st.ps, p);
-                                st.pu = shfl64(st.pu, p);
-                                fill = sl.upper ? 0xffffffffu : 0u;
-                            }
-                            const uint32_t m = temp < 32 ? ((1u << temp) - 1u) : 0xffffffffu;
-                            for (int w = 0; w < nwo; ++w) M.st(dl, op.dst_row + w, lane, fill & m);
-                        } else if (op.type == OP_SPC) {  // FastSC only
-                            uint32_t parity = 0;
-                            double best = 0;
-                            int bi = 0;
-                            for (int w = 0; w < nwo; ++w) {
-                                uint32_t word = 0;
-                                for (int i = 0; i < 32 && 32 * w + i < temp; ++i) {
-                                    const int j = 32 * w + i;
-                                    const double l = llr(j);
-                                    const uint32_t h = l <= 0;
-                                    word |= h << i;
-                                    parity ^= h;
-                                    const double a = fabs(l);
-                                    if (j == 0 || a < best) {  // first minimum (H6)
-                                        best = a;
-                                        bi = j;
-                                    }
-                                }
-                                M.st(dl, op.dst_row + w, lane, word);
-                            }
-                            if (parity) {
-                                const int row = op.dst_row + (bi >> 5);
-                                M.st(dl, row, lane, M.ld(dl, row, lane) ^ (1u << (bi & 31)));
-                            }
-                        } else if (!kList) {  // OP_R1, FastSC: `<= 0`
-                            for (int w = 0; w < nwo; ++w) {
-                                uint32_t word = 0;
-                                for (int i = 0; i < 32 && 32 * w + i < temp; ++i) word |= (uint32_t)(llr(32 * w + i) <= 0) << i;
-                                M.st(dl, op.dst_row + w, lane, word);
-                            }
-                        } else if constexpr (KIND == K_FASTSCL_LUT) {  // OP_R1, FastSCL: :99-166
-                            const int m = (L - 1) < temp ? (L - 1) : temp;
-                            uint32_t *g = M.gp;
-                            for (int w = 0; w < nwo; ++w) {
-                                uint32_t word = 0;
-                                for (int i = 0; i < 32 && 32 * w + i < temp; ++i) {
-                                    const int j = 32 * w + i;
-                                    const double l = llr(j);
-                                    word |= (uint32_t)(l < 0) << i;
-                                    ((double *)(g + (size_t)(P.K_row + 2 * j) * 64))[lane] = fabs(l);
-                                }
-                                g[(size_t)(P.H_row + w) * 64 + lane] = word;
-                            }
-                            int ord[kMaxM];
-                            double ms[kMaxM];
-                            int flip[kMaxM];
-    #pragma unroll
-                            for (int q = 0; q < kMaxM; ++q) {
-                                ord[q] = 0;
-                                ms[q] = 0;
-                                flip[q] = -1;
-                            }
-                            FastSortSeq seq{g, P.I_row, P.K_row, lane};
-                            if (temp <= stl::kThreshold) {
-                                uint32_t taken = 0;
-    #pragma unroll
-                                for (int q = 0; q < kMaxM; ++q) {
-                                    if (q < m) {
-                                        int bj = -1;
-                                        double bk = 0;
-                                        for (int j = 0; j < temp; ++j) {
-                                            if (taken & (1u << j)) continue;
-                                            const double kj = seq.key(j);
-                                            if (bj < 0 || kj < bk) {
-                                                bj = j;
-                                                bk = kj;
-                                            }
-                                        }
-                                        taken |= 1u << bj;
-                                        ord[q] = bj;
-                                        ms[q] = bk;
-                                    }
-                                }
-                            } else {
-                                for (int p = 0; p < temp; ++p) seq.set(p, p);
-                                stl::sort(seq, 0, temp);
-    #pragma unroll
-                                for (int q = 0; q < kMaxM; ++q) {
-                                    if (q < m) {
-                                        ord[q] = seq.get(q);
-                                        ms[q] = seq.key(ord[q]);
-                                    }
-                                }
-                            }
-                            wave_sync();  // H rows visible to the whole wave
-                            int origin = gl;
-    #pragma unroll
-                            for (int layer = 0; layer < kMaxM; ++layer) {
-                                if (layer < m) {
-                                    const double kf = st.pm + ms[layer];
-                                    const Sel sl = select_survivors(st.pm, kf, gl, gbase, L, sel);
-                                    const int p = gbase + sl.parent;
-                                    const int pos_old = ord[layer];  // H2
-                                    st.pm = pick(sl.upper, shfld(kf, p), shfld(st.pm, p));
-                                    st.ps = shfl64(st.ps, p);
-                                    st.pu = shfl64(st.pu, p);
-                                    origin = __shfl(origin, p);
-    #pragma unroll
-                                    for (int q = 0; q < kMaxM; ++q) {
-                                        ord[q] = __shfl(ord[q], p);
-                                        ms[q] = shfld(ms[q], p);
-                                        if (q < layer) flip[q] = __shfl(flip[q], p);
-                                    }
-                                    flip[layer] = sl.upper ? pos_old : -1;
-                                }
-                            }
-                            for (int w = 0; w < nwo; ++w) {
-                                uint32_t word = g[(size_t)(P.H_row + w) * 64 + gbase + origin];
-    #pragma unroll
-                                for (int q = 0; q < kMaxM; ++q)
-                                    if (q < m && flip[q] >= 0 && (flip[q] >> 5) == w) word ^= 1u << (flip[q] & 31);
-                                if (temp < 32) word &= (1u << temp) - 1u;
-                                M.st(dl, op.dst_row + w, lane, word);
-                            }
-                        }
-                    if (!(fl & MF_TO_R)) st.pu = pset(st.pu, op.sh_dst, gl);
+                    int *const sel = sel_all + sstride * s;
+                    special_op<kList, L8>(P, M, op, st, sel, gl, gbase, L, lane);
                   }
                   break;
                 }
@@ -836,7 +1007,7 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : QPD_WPE1) void lut_fast_ke
             __builtin_amdgcn_s_waitcnt(0);
             {
                 const uint64_t dt = __builtin_amdgcn_s_memtime() - stamp_t0;
-                const int cls = 2 * op.type + ((fl & MF_SYNC) ? 1 : 0);
+                const int cls = op.type == OP_R1 ? 24 + (op.cnt > 16) + (op.cnt > 8) : 2 * op.type + ((fl & MF_SYNC) ? 1 : 0);
                 if ((int)(threadIdx.x & 31) == cls) stamp_acc += dt;
                 if ((int)(threadIdx.x & 31) == cls) stamp_cnt += 1;
             }

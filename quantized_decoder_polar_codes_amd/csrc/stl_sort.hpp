@@ -197,6 +197,31 @@ QPD_HD void introsort_loop(Seq &s, int first, int last, int depth_limit) {
     }
 }
 
+// std::sort for last - first <= 2 * kThreshold + 1: a partition of a range
+// of at most 33 elements leaves at most one side above the threshold, so the
+// recursion of __introsort_loop degenerates into a loop and needs no stack
+// (same steps, same final array as sort()).
+template <class Seq>
+QPD_HD void sort_small(Seq &s, int first, int last) {
+    if (first == last) return;
+    int f = first, l = last, dl = lg(last - first) * 2;
+    while (l - f > kThreshold) {
+        if (dl == 0) {
+            heap_sort(s, f, l);
+            break;
+        }
+        --dl;
+        const int mid = f + (l - f) / 2;
+        move_median_to_first(s, f, f + 1, mid, l - 1);
+        const int cut = unguarded_partition(s, f + 1, l, f);
+        if (l - cut > kThreshold)
+            f = cut;  // the reference's recursion on [cut, l); [f, cut) is then too short to touch
+        else
+            l = cut;  // the reference's loop on [f, cut); [cut, l) was too short to touch
+    }
+    final_insertion_sort(s, first, last);
+}
+
 template <class Seq>
 QPD_HD void sort(Seq &s, int first, int last) {
     if (first == last) return;

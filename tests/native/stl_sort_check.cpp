@@ -22,6 +22,7 @@ int main(int argc, char **argv) {
     for (long t = 0; t < trials; ++t) {
         int n = 1 + rng() % 300;
         if (t % 3 == 0) n = 17 + rng() % 48;  // the R1-node sizes of interest
+        if (t % 3 == 1) n = 1 + rng() % 33;   // sort_small's range
         int distinct = 1 + rng() % 8;
         std::vector<double> key(n);
         for (auto &k : key) k = (double)(rng() % distinct) * 0.5;
@@ -36,6 +37,13 @@ int main(int argc, char **argv) {
         qpd::stl::sort(s, 0, n);
         if (a != b) {
             if (++bad < 5) printf("mismatch n=%d distinct=%d\n", n, distinct);
+        }
+        if (n <= 2 * qpd::stl::kThreshold + 1) {  // the stack-free form used on the device for R1 <= 32
+            std::vector<int> c(n);
+            for (int i = 0; i < n; ++i) c[i] = i;
+            VecSeq s2{c, key};
+            qpd::stl::sort_small(s2, 0, n);
+            if (a != c && ++bad < 5) printf("sort_small mismatch n=%d distinct=%d\n", n, distinct);
         }
     }
     printf("trials=%ld mismatches=%ld\n", trials, bad);

@@ -325,6 +325,30 @@ def test_fast_engine_lds_placement_sweep(qpd, oracle_mod, monkeypatch):
         assert len(seen) >= 4
 
 
+@pytest.mark.parametrize("N,K,L", [(256, 128, 8), (512, 420, 5), (1024, 900, 8)])
+def test_fastscl_rate1_paths(N, K, L, qpd, oracle_mod, monkeypatch):
+    """FastSCL rate-1 nodes through all three argsort paths: <= 16 elements in
+    registers, 17..32 in the LDS tail (default budget) or, with the tree in
+    global scratch (budget 256), the slab path, and > 32 elements (a 256-element
+    node at N = 1024, K = 900) -- tie-heavy tables so the introsort replay
+    matters."""
+    from quantized_decoder_polar_codes_amd import lut as LU
+
+    p = LU.random_luts(N, 16, seed=N + K, distinct_mags=3)
+    fm, nt = _node_type(N, K)
+    sym = np.random.default_rng(N - K).integers(0, 16, size=(48, N), dtype=np.int32)
+    want = oracle_mod.decode_lut("FastSCL-LUT", p, K, L, fm, sym, node_type=nt)
+    for budget in (None, 256):
+        if budget is None:
+            monkeypatch.delenv("QPD_LDS_BUDGET", raising=False)
+        else:
+            monkeypatch.setenv("QPD_LDS_BUDGET", str(budget))
+        d = qpd.from_packed("FastSCL-LUT", p, K, fm, L=L, node_type=nt, engine="fast")
+        got = d.decode_batch(sym)
+        bad = np.flatnonzero((got != want).any(1))
+        assert bad.size == 0, (budget, bad[:5])
+
+
 def test_fast_engine_rejects_per_element_tables(qpd):
     from quantized_decoder_polar_codes_amd import lut as LU
 

@@ -15,12 +15,9 @@ from quantized_decoder_polar_codes_amd import _lib, codes as C, lut as LU  # noq
 kind = sys.argv[1] if len(sys.argv) > 1 else "SCL-LUT"
 N, K, L, F = (int(x) for x in sys.argv[2:6]) if len(sys.argv) > 5 else (1024, 512, 8, 262144)
 names = ["F", "G", "LEAF_L", "LEAF_R", "COMB", "R0", "R1", "REP", "SPC", "BOT3"]
-_, mb, fm, mm = C.construct_pw(N, K)
-nt = C.identify_nodes(N, mb).astype(np.int32)
-p = LU.minsum_uniform_luts(N)
-rng = np.random.default_rng(0)
-sym = torch.from_numpy(rng.integers(3, 13, size=(F, N), dtype=np.int32)).cuda()
-d = Q.from_packed(kind, p, K, fm, L=L, node_type=nt)
+import bench  # noqa: E402
+
+d, _, fm, nt, _, sym = bench.workload(N, K, L, kind, F, 2.0)  # the bench workload (MinDistortion, 2 dB)
 lib = _lib.load()
 buf = (ctypes.c_ulonglong * 64)()
 d.decode_batch(sym)
@@ -43,6 +40,7 @@ print(f"total stamped wave-cycles per task {tot / tasks:,.0f}")
 for c in range(32):
     if cnt[c] == 0:
         continue
-    nm = "TAIL" if c == 31 else names[c // 2] + ("/sync" if c % 2 else "")
+    nm = "TAIL" if c == 31 else ({24: "R1<=8", 25: "R1 9-16", 26: "R1>16"}[c] if 24 <= c <= 26 else
+                                  names[c // 2] + ("/sync" if c % 2 else ""))
     print(f"  {nm:12s} ops/task {cnt[c] / tasks:8.1f}  cyc/op {acc[c] / cnt[c]:9.0f}  cyc/task {acc[c] / tasks:11,.0f}  "
           f"{100 * acc[c] / tot:5.1f}%")
