@@ -16,8 +16,12 @@ OUT="$HERE/_ref"
 mkdir -p "$OUT"
 SUFFIX="$(python3-config --extension-suffix)"
 TARGET="$OUT/_refPolarDecoder$SUFFIX"
-SRCS="utils SCDecoder SCLUTDecoder SCLLUTDecoder FastSCLUT FastSCLLUTDecoder CASCLLUTDecoder CAFastSCLLUTDecoder"
-PYI="py_SCDecoder py_SCLUTDecoder py_SCLLUTDecoder py_FastSCLUTDecoder py_FastSCLLUTDecoder py_CASCLLUTDecoder py_CAFastSCLLUTDecoder"
+SRCS="utils SCDecoder SCLUTDecoder SCLLUTDecoder FastSCLUT FastSCLLUTDecoder CASCLLUTDecoder CAFastSCLLUTDecoder
+      SCLDecoder CASCLDecoder FastSCDecoder FastSCLDecoder SCUniformQuantizedDecoder SCLUniformQuantizedDecoder
+      SCLloydQuantizedDecoder SCLLloydQuantizedDecoder"
+PYI="py_SCDecoder py_SCLUTDecoder py_SCLLUTDecoder py_FastSCLUTDecoder py_FastSCLLUTDecoder py_CASCLLUTDecoder py_CAFastSCLLUTDecoder
+     py_SCLDecoder py_CASCLDecoder py_FastSCDecoder py_FastSCLDecoder py_SCUniformDecoder py_SCLUniformQuantizedDecoder
+     py_SCLloydQuantizedDecoder py_SCLLloydQuantizedDecoder"
 FILES=""
 for s in $SRCS; do FILES="$FILES $R/src/$s.cpp"; done
 for s in $PYI; do FILES="$FILES $R/py_interface/$s.cpp"; done

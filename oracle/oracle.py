@@ -45,6 +45,9 @@ def lib():
         L.orc_decode_lut_ca.restype = ctypes.c_int
         L.orc_decode_sc_float.argtypes = [i32, i32, P, P, i64, P]
         L.orc_decode_sc_float.restype = ctypes.c_int
+        L.orc_decode_float.argtypes = [i32, i32, i32, i32, P, P, i32, P, P, P, P, P, P, P, P, i32, i32, P, i32, P,
+                                       i64, P]
+        L.orc_decode_float.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -118,6 +121,40 @@ def decode_sc_float(N: int, K: int, frozen, llr) -> np.ndarray:
     out = np.zeros((x.shape[0], K), dtype=np.uint8)
     frozen = np.ascontiguousarray(np.asarray(frozen, dtype=np.int32))
     rc = lib().orc_decode_sc_float(N, K, _ptr(frozen), _ptr(x), x.shape[0], _ptr(out))
+    if rc != 0:
+        raise RuntimeError(f"oracle decode failed rc={rc}")
+    return out
+
+
+# Float-domain kinds (include/qpd.h enum qpd_kind)
+FLOAT_KIND = {"SC": 0, "SCL": 7, "CA-SCL": 8, "FastSC": 9, "FastSCL": 10, "SC-Uniform": 11, "SCL-Uniform": 12,
+              "SC-Lloyd": 13, "SCL-Lloyd": 14}
+
+
+def decode_float(kind: str, N: int, K: int, frozen, llr, L: int = 1, node_type=None, quant=None, A: int = 0,
+                 crc_n: int = 0, crc_loc=()) -> np.ndarray:
+    """Restated float-domain decoder ``kind`` on float64 LLRs [B, N] -> uint8 [B, K] ([B, A] for CA-SCL).
+    ``quant``: quant.UniformQuant (Uniform kinds) or quant.LloydQuant (Lloyd kinds)."""
+    k = FLOAT_KIND[kind]
+    x = np.ascontiguousarray(np.asarray(llr, dtype=np.float64).reshape(-1, N))
+    B = x.shape[0]
+    ob = A if kind == "CA-SCL" else K
+    out = np.zeros((B, ob), dtype=np.uint8)
+    frozen = np.ascontiguousarray(np.asarray(frozen, dtype=np.int32))
+    nt = None if node_type is None else np.ascontiguousarray(np.asarray(node_type).astype(np.int32))
+    loc = np.ascontiguousarray(np.asarray(crc_loc, dtype=np.int32))
+    v = 0
+    rf = rg = bnd = boff = blen = rec = roff = rlen = None
+    if quant is not None:
+        v = quant.v
+        if hasattr(quant, "r_f"):
+            rf, rg = quant.r_f, quant.r_g
+        else:
+            bnd, boff, blen, rec, roff, rlen = (quant.bnd, quant.bnd_off, quant.bnd_len, quant.rec, quant.rec_off,
+                                                quant.rec_len)
+    rc = lib().orc_decode_float(k, N, K, L, _ptr(frozen), _ptr(nt), v, _ptr(rf), _ptr(rg), _ptr(bnd), _ptr(boff),
+                                _ptr(blen), _ptr(rec), _ptr(roff), _ptr(rlen), A, crc_n, _ptr(loc), loc.size,
+                                _ptr(x), B, _ptr(out))
     if rc != 0:
         raise RuntimeError(f"oracle decode failed rc={rc}")
     return out

@@ -1,5 +1,5 @@
 // =============================================================================
-// qpd_oracle.cpp -- CPU restatement of the reference LUT polar decoders.
+// qpd_oracle.cpp -- CPU restatement of the reference polar decoders.
 //
 // TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the HIP
 // product path and the `cpu_baseline` leg of bench.py.  Nothing in
@@ -15,9 +15,18 @@
 //   CA-SCL-LUT      .../src/CASCLLUTDecoder.cpp:47-303   (CRC epilogue :263-302)
 //   CA-FastSCL-LUT  .../src/CAFastSCLLUTDecoder.cpp:57-454 (CRC epilogue :332-453)
 //   CRC::encoding   .../src/utils.cpp:77-92
+//   SCL (float)     .../src/SCLDecoder.cpp:38-176
+//   CA-SCL (float)  .../src/CASCLDecoder.cpp:56-249
+//   FastSC (float)  .../src/FastSCDecoder.cpp:21-174
+//   FastSCL (float) .../src/FastSCLDecoder.cpp:49-423
+//   SC/SCL uniform  .../src/SC{,L}UniformQuantizedDecoder.cpp (Q utils.cpp:8-10)
+//   SC/SCL Lloyd    .../src/SC{,L}{l,L}loydQuantizedDecoder.cpp (bisect utils.cpp:12-24)
 //   partial sums    .../src/utils.cpp:62-67 (u), min-sum f/g utils.cpp:26-36
 //
-// It keeps the reference's per-fork deep copies of the whole list state, so
+// One template per decoder family (SCDec / SCLDec) over a symbol domain
+// (LutDom: int symbols + tables; FloatDom: fp64 LLRs, min-sum, optional
+// uniform / Lloyd re-quantization), since the reference's 15 classes differ
+// only in those two respects.  It keeps the reference's per-fork deep copies of the whole list state, so
 // that its speed is representative of the reference CPU decoder (SURVEY.md
 // §8(d)), and it calls libstdc++ std::sort with the same comparator as the
 // reference so that tie order is identical (hazard H1).  Parity is pinned by
@@ -123,6 +132,8 @@ std::vector<uint8_t> crc_encoding(const std::vector<uint8_t> &info, int crc_n, c
 // wins, else the first in that order.
 struct CaSpec {
     int A = 0, crc_n = 0;
+    int nchk = 0;  // bits compared after the A info bits: K - A (LUT kinds,
+                   // CASCLLUTDecoder.cpp:279) or crc_n (CASCLDecoder.cpp:223)
     std::vector<int> p;  // crc_n + 1 coefficients
 };
 
@@ -131,85 +142,126 @@ int first_argmin(const std::vector<double> &x) {
 }
 
 // ---------------------------------------------------------------------------
-// SC (float, min-sum) -- SCDecoder.cpp:14-89, f/g utils.cpp:26-36
+// Symbol domains.  The reference's decoders differ only in what a tree node
+// holds and how f/g and a node's LLR are formed:
+//   LutDom   -- int symbols, f/g by per-node tables, LLR = vcl[row][pos][sym]
+//               (SCLUTDecoder.cpp:83-97, hazard H3: row depth-1)
+//   FloatDom -- fp64 LLRs, min-sum f/g (utils.cpp:26-36), optionally
+//               re-quantized after every f/g: uniform Q (utils.cpp:8-10,
+//               q_f/q_g :38-48, SCUniformQuantizedDecoder.cpp:55-57,71-73) or
+//               Lloyd bisect (utils.cpp:12-24, non_uniform_q_f/g :50-60,
+//               SCLloydQuantizedDecoder.cpp:57-59,73-75); LLR = the value.
 // ---------------------------------------------------------------------------
-struct FloatSC {
+int sgn(double x) { return x < 0 ? -1 : (x > 0); }  // utils.h:13
+
+struct LutDom {
+    using T = int;
     const Code &c;
-    std::vector<double> alpha;
-    std::vector<uint8_t> beta;
-    explicit FloatSC(const Code &c_) : c(c_), alpha((c_.n + 1) * c_.N), beta((c_.n + 1) * c_.N) {}
+    T f(int posi, int j, T a, T b) const { return c.F(posi, j, a, b); }
+    T g(int posi, int j, int u, T a, T b) const { return c.G(posi, j, u, a, b); }
+    double llr(int row, int pos, T s) const { return c.Q(row, pos, s); }
+    bool bad() const { return false; }
+};
 
-    static int sgn(double x) { return x < 0 ? -1 : (x > 0); }
+enum Quant { Q_NONE = 0, Q_UNIFORM = 1, Q_LLOYD = 2 };
 
-    void leaf(int k) {
-        const int N = c.N, n = c.n;
-        beta[n * N + k] = c.frozen[k] == 1 ? 0 : (uint8_t)(alpha[n * N + k] <= 0);
+struct FloatDom {
+    using T = double;
+    int quant = Q_NONE;
+    int v = 0;
+    const double *r_f = nullptr, *r_g = nullptr;  // uniform step per node_posi
+    // Lloyd: table t (0 = f, 1 = g) of node p is bnd[bnd_off[t*(N-1)+p] ...
+    // + bnd_len[...]) and rec[rec_off[...] ... + rec_len[...])
+    const double *bnd = nullptr, *rec = nullptr;
+    const int32_t *bnd_off = nullptr, *bnd_len = nullptr, *rec_off = nullptr, *rec_len = nullptr;
+    int nodes = 0;
+    mutable bool ub = false;  // a Lloyd index outside the reconstruction (reference UB)
+
+    static double Q(double x, double r, double M) {  // utils.cpp:8-10
+        return std::fabs(x) > M ? sgn(x) * (M - 0.5 * r) : (std::floor(x / r) + 0.5) * r;
     }
-    void visit(int d, int node) {
-        const int N = c.N, n = c.n;
-        if (d == n) { leaf(node); return; }
-        const int temp = N >> d, half = temp / 2;
-        const double *a = &alpha[d * N + temp * node];
-        const double *b = a + half;
-        double *lo = &alpha[(d + 1) * N + half * (2 * node)];
-        for (int j = 0; j < half; ++j)
-            lo[j] = (sgn(a[j]) * sgn(b[j])) * std::min(std::fabs(a[j]), std::fabs(b[j]));
-        visit(d + 1, 2 * node);
-        const uint8_t *ul = &beta[(d + 1) * N + half * (2 * node)];
-        double *hi = &alpha[(d + 1) * N + half * (2 * node + 1)];
-        for (int j = 0; j < half; ++j) hi[j] = (1 - 2 * ul[j]) * a[j] + b[j];
-        visit(d + 1, 2 * node + 1);
-        combine(&beta[d * N + temp * node], ul, &beta[(d + 1) * N + half * (2 * node + 1)], half);
+    double bisect(double a, int t, int posi) const {  // utils.cpp:12-24
+        const double *b = bnd + bnd_off[t * nodes + posi];
+        int lo = 0, hi = bnd_len[t * nodes + posi];
+        while (lo < hi) {
+            int mid = (lo + hi) / 2;
+            if (b[mid] < a)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        if (lo - 1 < 0 || lo - 1 >= rec_len[t * nodes + posi]) {
+            ub = true;
+            return 0.0;
+        }
+        return rec[rec_off[t * nodes + posi] + lo - 1];
     }
-    void run(const double *llr, uint8_t *out) {
-        std::memcpy(alpha.data(), llr, sizeof(double) * c.N);
-        visit(0, 0);
-        emit_info(c, &beta[c.n * c.N], out);
+    T f(int posi, int, T a, T b) const {
+        const double x = (sgn(a) * sgn(b)) * std::min(std::fabs(a), std::fabs(b));
+        if (quant == Q_UNIFORM) return Q(x, r_f[posi], double(v / 2 - 0.5) * r_f[posi]);
+        if (quant == Q_LLOYD) return bisect(x, 0, posi);
+        return x;
     }
+    T g(int posi, int, int u, T a, T b) const {
+        const double x = (1 - 2 * u) * a + b;
+        if (quant == Q_UNIFORM) return Q(x, r_g[posi], double(v / 2 - 1) * r_g[posi]);
+        if (quant == Q_LLOYD) return bisect(x, 1, posi);
+        return x;
+    }
+    double llr(int, int, T s) const { return s; }
+    bool bad() const { return ub; }
 };
 
 // ---------------------------------------------------------------------------
-// SC-LUT -- SCLUTDecoder.cpp:21-124 (and the non-special part of
-// FastSCLUT.cpp:27-206 when `fast` is set).
+// SC family: SC (SCDecoder.cpp:14-89), SC-LUT (SCLUTDecoder.cpp:21-124),
+// SC uniform/Lloyd (SCUniformQuantizedDecoder.cpp:20-99,
+// SCLloydQuantizedDecoder.cpp:22-101), and with `fast` FastSC-LUT
+// (FastSCLUT.cpp:27-206) / FastSC (FastSCDecoder.cpp:21-174).
 // ---------------------------------------------------------------------------
-struct LutSC {
+template <class D>
+struct SCDec {
+    using T = typename D::T;
     const Code &c;
+    const D &dom;
     bool fast;
-    std::vector<int> sym;
+    std::vector<T> sym;
     std::vector<uint8_t> ucap;
-    LutSC(const Code &c_, bool fast_) : c(c_), fast(fast_), sym((c_.n + 1) * c_.N), ucap((c_.n + 1) * c_.N) {}
+    SCDec(const Code &c_, const D &dom_, bool fast_)
+        : c(c_), dom(dom_), fast(fast_), sym((c_.n + 1) * c_.N), ucap((c_.n + 1) * c_.N) {}
 
-    // Leaf decision from a node at depth n-1 (SCLUTDecoder.cpp:59-66, 90-97).
-    // Hazard H4: SC family decides `llr <= 0`.  Frozen leaves skip the LUT.
-    void leaf(int posi, int k, bool right, const int *pa, const int *pb, int ul) {
+    // Leaf decision from a node at depth n-1 (SCLUTDecoder.cpp:59-66, 90-97;
+    // SCDecoder.cpp:24-29).  Hazard H4: SC family decides `llr <= 0`.
+    // Frozen leaves are 0 whatever the LLR.
+    void leaf(int posi, int k, bool right, const T *pa, const T *pb, int ul) {
         const int N = c.N, n = c.n;
         if (c.frozen[k] == 1) { ucap[n * N + k] = 0; return; }
-        int s = right ? c.G(posi, 0, ul, pa[0], pb[0]) : c.F(posi, 0, pa[0], pb[0]);
-        ucap[n * N + k] = (uint8_t)(c.Q(n - 1, k, s) <= 0);
+        T s = right ? dom.g(posi, 0, ul, pa[0], pb[0]) : dom.f(posi, 0, pa[0], pb[0]);
+        ucap[n * N + k] = (uint8_t)(dom.llr(n - 1, k, s) <= 0);
     }
 
-    // Special nodes of FastSC-LUT, FastSCLUT.cpp:46-107.  vcl row depth-1 (H3).
+    // Special nodes, FastSCLUT.cpp:46-107 / FastSCDecoder.cpp:45-106.  LUT
+    // domain: vcl row depth-1 (H3).
     bool special(int d, int node) {
         const int N = c.N;
         const int posi = (1 << d) + node - 1;
         const int t = c.type(posi);
         if (!fast || t < 0 || t > 3) return false;
         const int temp = N >> d;
-        const int *ps = &sym[d * N + temp * node];
+        const T *ps = &sym[d * N + temp * node];
         uint8_t *pu = &ucap[d * N + temp * node];
         if (t == 0) {  // R0, :46-54
             std::memset(pu, 0, temp);
         } else if (t == 1) {  // R1, :55-66
-            for (int i = 0; i < temp; ++i) pu[i] = c.Q(d - 1, temp * node + i, ps[i]) <= 0;
+            for (int i = 0; i < temp; ++i) pu[i] = dom.llr(d - 1, temp * node + i, ps[i]) <= 0;
         } else if (t == 2) {  // REP, :67-80 (sequential fp64 sum, H5)
             double S = 0;
-            for (int i = 0; i < temp; ++i) S += c.Q(d - 1, temp * node + i, ps[i]);
+            for (int i = 0; i < temp; ++i) S += dom.llr(d - 1, temp * node + i, ps[i]);
             std::memset(pu, (uint8_t)(S <= 0), temp);
         } else {  // SPC, :81-107 (first-min flip, H6)
             std::vector<double> mag(temp);
             int parity = 0;
             for (int i = 0; i < temp; ++i) {
-                double l = c.Q(d - 1, temp * node + i, ps[i]);
+                double l = dom.llr(d - 1, temp * node + i, ps[i]);
                 pu[i] = (uint8_t)(l <= 0);
                 parity += pu[i];
                 mag[i] = std::fabs(l);
@@ -227,20 +279,20 @@ struct LutSC {
         if (special(d, node)) return;
         const int posi = (1 << d) + node - 1;
         const int temp = N >> d, half = temp / 2;
-        const int *pa = &sym[d * N + temp * node];
-        const int *pb = pa + half;
+        const T *pa = &sym[d * N + temp * node];
+        const T *pb = pa + half;
         const int l = 2 * node, r = 2 * node + 1;
         if (d + 1 < n) {
-            int *lo = &sym[(d + 1) * N + half * l];
-            for (int j = 0; j < half; ++j) lo[j] = c.F(posi, j, pa[j], pb[j]);
+            T *lo = &sym[(d + 1) * N + half * l];
+            for (int j = 0; j < half; ++j) lo[j] = dom.f(posi, j, pa[j], pb[j]);
             visit(d + 1, l);
         } else {
             leaf(posi, l, false, pa, pb, 0);
         }
         const uint8_t *ul = &ucap[(d + 1) * N + half * l];
         if (d + 1 < n) {
-            int *hi = &sym[(d + 1) * N + half * r];
-            for (int j = 0; j < half; ++j) hi[j] = c.G(posi, j, ul[j], pa[j], pb[j]);
+            T *hi = &sym[(d + 1) * N + half * r];
+            for (int j = 0; j < half; ++j) hi[j] = dom.g(posi, j, ul[j], pa[j], pb[j]);
             visit(d + 1, r);
         } else {
             leaf(posi, r, true, pa, pb, ul[0]);
@@ -248,11 +300,13 @@ struct LutSC {
         combine(&ucap[d * N + temp * node], ul, &ucap[(d + 1) * N + half * r], half);
     }
 
-    int run(const int32_t *y, uint8_t *out) {
+    template <class In>
+    int run(const In *y, uint8_t *out) {
         const int N = c.N, n = c.n;
         if (fast && c.type(0) >= 0 && c.type(0) <= 3) return -2;  // reference UB (root special)
-        for (int i = 0; i < N; ++i) sym[i] = y[i];
+        for (int i = 0; i < N; ++i) sym[i] = (T)y[i];
         visit(0, 0);
+        if (dom.bad()) return -4;
         if (!fast) {
             emit_info(c, &ucap[n * N], out);  // SCLUTDecoder.cpp:116-123
         } else {
@@ -265,21 +319,28 @@ struct LutSC {
 };
 
 // ---------------------------------------------------------------------------
-// SCL-LUT -- SCLLUTDecoder.cpp:47-253, and FastSCL-LUT (FastSCLLUTDecoder.cpp:
-// 57-408) when `fast` is set.  State is L full copies of the symbol tree and
+// SCL family: SCL-LUT (SCLLUTDecoder.cpp:47-253), SCL (SCLDecoder.cpp:38-176),
+// SCL uniform/Lloyd (SCLUniformQuantizedDecoder.cpp:43-184,
+// SCLLloydQuantizedDecoder.cpp:46-187), CA-SCL (CASCLDecoder.cpp:74-249), and
+// with `fast` FastSCL-LUT (FastSCLLUTDecoder.cpp:57-408) / FastSCL
+// (FastSCLDecoder.cpp:49-423).  State is L full copies of the node values and
 // partial sums, deep-copied at every fork exactly as the reference does.
 // ---------------------------------------------------------------------------
-struct LutSCL {
+template <class D>
+struct SCLDec {
+    using T = typename D::T;
     const Code &c;
+    const D &dom;
     bool fast;
     int L;
-    std::vector<std::vector<int>> sym;
+    double pm_init = kInf;  // DOUBLE_INF: 1.0/0.0 (LUT kinds, FastSCL), 1e300 (SCLDecoder.h:8 ...)
+    std::vector<std::vector<T>> sym;
     std::vector<std::vector<uint8_t>> ucap;
     std::vector<double> pm;
 
     CaSpec ca;  // ca.A > 0: CRC-aided output of A bits
 
-    LutSCL(const Code &c_, bool fast_) : c(c_), fast(fast_), L(c_.L) {}
+    SCLDec(const Code &c_, const D &dom_, bool fast_) : c(c_), dom(dom_), fast(fast_), L(c_.L) {}
 
     // Keep L survivors of the 2L candidates `pm2` (mink, :8-21).  Returns the
     // parent path and whether the candidate came from the upper half.
@@ -294,7 +355,7 @@ struct LutSCL {
         }
     }
     void permute(const std::vector<int> &parent) {
-        std::vector<std::vector<int>> s2(L);
+        std::vector<std::vector<T>> s2(L);
         std::vector<std::vector<uint8_t>> u2(L);
         for (int i = 0; i < L; ++i) {
             s2[i] = sym[parent[i]];
@@ -311,10 +372,10 @@ struct LutSCL {
         const int temp = N >> d, half = temp / 2;
         std::vector<double> dm(L);
         for (int i = 0; i < L; ++i) {
-            const int *p = &sym[i][d * N + temp * node];
-            int s = right ? c.G(posi, 0, ucap[i][(d + 1) * N + half * (2 * node)], p[0], p[half])
-                          : c.F(posi, 0, p[0], p[half]);
-            dm[i] = c.Q(n - 1, k, s);
+            const T *p = &sym[i][d * N + temp * node];
+            T s = right ? dom.g(posi, 0, ucap[i][(d + 1) * N + half * (2 * node)], p[0], p[half])
+                        : dom.f(posi, 0, p[0], p[half]);
+            dm[i] = dom.llr(n - 1, k, s);
         }
         if (c.frozen[k] == 1) {
             for (int i = 0; i < L; ++i) {
@@ -340,8 +401,10 @@ struct LutSCL {
         }
     }
 
-    // FastSCL-LUT special nodes, FastSCLLUTDecoder.cpp:82-213.  SPC (type 3)
-    // has no handler in the reference (:215 TODO) and falls through (H7).
+    // FastSCL special nodes, FastSCLLUTDecoder.cpp:82-213 /
+    // FastSCLDecoder.cpp:122-251.  SPC (type 3) has no handler in either
+    // reference (LUT :215 TODO; float :253-345 commented out) and falls
+    // through (H7).
     bool special(int d, int node) {
         const int N = c.N;
         const int posi = (1 << d) + node - 1;
@@ -353,7 +416,7 @@ struct LutSCL {
             for (int i = 0; i < L; ++i) {
                 std::memset(&ucap[i][off], 0, temp);
                 for (int j = 0; j < temp; ++j) {
-                    double l = c.Q(d - 1, temp * node + j, sym[i][off + j]);
+                    double l = dom.llr(d - 1, temp * node + j, sym[i][off + j]);
                     pm[i] += (float)(l < 0) * std::fabs(l);
                 }
             }
@@ -364,7 +427,7 @@ struct LutSCL {
             std::vector<std::vector<int>> order(L);
             for (int i = 0; i < L; ++i) {
                 for (int j = 0; j < temp; ++j) {
-                    double l = c.Q(d - 1, temp * node + j, sym[i][off + j]);
+                    double l = dom.llr(d - 1, temp * node + j, sym[i][off + j]);
                     dec[i][j] = (uint8_t)(l < 0);
                     mag[i][j] = std::fabs(l);
                 }
@@ -407,7 +470,7 @@ struct LutSCL {
             }
             for (int i = 0; i < L; ++i) {
                 for (int j = 0; j < temp; ++j) {
-                    double l = c.Q(d - 1, temp * node + j, sym[i][off + j]);
+                    double l = dom.llr(d - 1, temp * node + j, sym[i][off + j]);
                     pm2[i] += (double)(l < 0) * std::fabs(l);
                     pm2[i + L] += (double)(l >= 0) * std::fabs(l);
                 }
@@ -431,9 +494,9 @@ struct LutSCL {
         // f (:83-90 / :223-230)
         if (d + 1 < n) {
             for (int i = 0; i < L; ++i) {
-                int *s = sym[i].data();
+                T *s = sym[i].data();
                 for (int j = 0; j < half; ++j)
-                    s[(d + 1) * N + half * l + j] = c.F(posi, j, s[off + j], s[off + half + j]);
+                    s[(d + 1) * N + half * l + j] = dom.f(posi, j, s[off + j], s[off + half + j]);
             }
             visit(d + 1, l);
         } else {
@@ -442,10 +505,10 @@ struct LutSCL {
         // g (:157-165 / :297-305)
         if (d + 1 < n) {
             for (int i = 0; i < L; ++i) {
-                int *s = sym[i].data();
+                T *s = sym[i].data();
                 const uint8_t *ul = &ucap[i][(d + 1) * N + half * l];
                 for (int j = 0; j < half; ++j)
-                    s[(d + 1) * N + half * r + j] = c.G(posi, j, ul[j], s[off + j], s[off + half + j]);
+                    s[(d + 1) * N + half * r + j] = dom.g(posi, j, ul[j], s[off + j], s[off + half + j]);
             }
             visit(d + 1, r);
         } else {
@@ -456,16 +519,20 @@ struct LutSCL {
             combine(&ucap[i][off], &ucap[i][(d + 1) * N + half * l], &ucap[i][(d + 1) * N + half * r], half);
     }
 
-    int run(const int32_t *y, uint8_t *out) {
+    template <class In>
+    int run(const In *y, uint8_t *out) {
         const int N = c.N, n = c.n;
         if (fast && c.type(0) >= 0 && c.type(0) <= 2) return -2;  // reference UB (root special)
-        sym.assign(L, std::vector<int>((n + 1) * N));
+        sym.assign(L, std::vector<T>((n + 1) * N));
         ucap.assign(L, std::vector<uint8_t>((n + 1) * N));
-        pm.assign(L, kInf);
+        pm.assign(L, pm_init);
         pm[0] = 0;
         for (int i = 0; i < L; ++i)
-            for (int k = 0; k < N; ++k) sym[i][k] = y[k];
+            for (int k = 0; k < N; ++k) sym[i][k] = (T)y[k];
         visit(0, 0);
+        if (dom.bad()) return -4;
+        for (double p : pm)
+            if (std::isnan(p)) return -4;  // NaN keys: std::sort's order is undefined
         if (ca.A > 0) {
             // decoded info bits of a path: ucap[n] (SCL, :268-275) or the re-encoded
             // root partial sums (FastSCL, :338-355)
@@ -484,7 +551,7 @@ struct LutSCL {
                 std::vector<uint8_t> head(info.begin(), info.begin() + ca.A);
                 std::vector<uint8_t> chk = crc_encoding(head, ca.crc_n, ca.p);
                 bool pass = true;
-                for (int j = 0; j < c.K - ca.A; ++j)
+                for (int j = 0; j < ca.nchk; ++j)
                     if (chk[j] != info[ca.A + j]) {
                         pass = false;
                         break;
@@ -545,8 +612,9 @@ int orc_decode_lut(int32_t kind, int32_t N, int32_t K, int32_t L, int32_t v, con
     Code c = make_code(N, K, kind == 2 || kind == 4 ? L : 1, v, frozen, node_type, lut_f, f_base, f_step, lut_g,
                        g_base, g_step, vcl, vcl_rows);
     if (N < 2 || (1 << c.n) != N) return -1;
+    LutDom dom{c};
     if (kind == 1 || kind == 3) {
-        LutSC dec(c, kind == 3);
+        SCDec<LutDom> dec(c, dom, kind == 3);
         for (int64_t b = 0; b < B; ++b) {
             int rc = dec.run(sym + b * N, out + b * K);
             if (rc) return rc;
@@ -554,7 +622,7 @@ int orc_decode_lut(int32_t kind, int32_t N, int32_t K, int32_t L, int32_t v, con
         return 0;
     }
     if (kind == 2 || kind == 4) {
-        LutSCL dec(c, kind == 4);
+        SCLDec<LutDom> dec(c, dom, kind == 4);
         for (int64_t b = 0; b < B; ++b) {
             int rc = dec.run(sym + b * N, out + b * K);
             if (rc) return rc;
@@ -576,9 +644,11 @@ int orc_decode_lut_ca(int32_t kind, int32_t N, int32_t K, int32_t A, int32_t L, 
     if (A < 1 || A > K || K - A > crc_n) return -1;
     Code c = make_code(N, K, L, v, frozen, node_type, lut_f, f_base, f_step, lut_g, g_base, g_step, vcl, vcl_rows);
     if (N < 2 || (1 << c.n) != N) return -1;
-    LutSCL dec(c, kind == 4);
+    LutDom dom{c};
+    SCLDec<LutDom> dec(c, dom, kind == 4);
     dec.ca.A = A;
     dec.ca.crc_n = crc_n;
+    dec.ca.nchk = K - A;
     dec.ca.p.assign(crc_n + 1, 0);
     for (int i = 0; i < n_loc; ++i) dec.ca.p[crc_loc[i]] = 1;
     for (int64_t b = 0; b < B; ++b) {
@@ -592,8 +662,78 @@ int orc_decode_lut_ca(int32_t kind, int32_t N, int32_t K, int32_t A, int32_t L, 
 int orc_decode_sc_float(int32_t N, int32_t K, const int32_t *frozen, const double *llr, int64_t B, uint8_t *out) {
     Code c = make_code(N, K, 1, 1, frozen, nullptr, nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr, 0);
     if (N < 2 || (1 << c.n) != N) return -1;
-    FloatSC dec(c);
+    FloatDom dom;
+    SCDec<FloatDom> dec(c, dom, false);
     for (int64_t b = 0; b < B; ++b) dec.run(llr + b * N, out + b * K);
+    return 0;
+}
+
+// Float-domain decoders on float64 LLRs [B][N] (kinds as include/qpd.h):
+//   0 SC            SCDecoder.cpp:14-89
+//   7 SCL           SCLDecoder.cpp:38-176              (PM init 1e300, SCLDecoder.h:8)
+//   8 CA-SCL        CASCLDecoder.cpp:74-249            (1e300; CRC from crc_n/crc_loc,
+//                                                       crc_n bits compared, :202-235)
+//   9 FastSC        FastSCDecoder.cpp:21-174
+//  10 FastSCL       FastSCLDecoder.cpp:49-423          (PM init 1.0/0.0, FastSCLDecoder.h:7)
+//  11 SC-Uniform    SCUniformQuantizedDecoder.cpp:20-99
+//  12 SCL-Uniform   SCLUniformQuantizedDecoder.cpp:43-184 (1e300)
+//  13 SC-Lloyd      SCLloydQuantizedDecoder.cpp:22-101
+//  14 SCL-Lloyd     SCLLloydQuantizedDecoder.cpp:46-187   (1e300)
+// Output uint8 [B][K] ([B][A] for kind 8).  Returns -4 where the reference's
+// behaviour is undefined (Lloyd index outside the reconstruction, NaN path
+// metrics).
+int orc_decode_float(int32_t kind, int32_t N, int32_t K, int32_t L, const int32_t *frozen, const int32_t *node_type,
+                     int32_t v, const double *r_f, const double *r_g, const double *bnd, const int32_t *bnd_off,
+                     const int32_t *bnd_len, const double *rec, const int32_t *rec_off, const int32_t *rec_len,
+                     int32_t A, int32_t crc_n, const int32_t *crc_loc, int32_t n_loc, const double *llr, int64_t B,
+                     uint8_t *out) {
+    const bool list = kind == 7 || kind == 8 || kind == 10 || kind == 12 || kind == 14;
+    const bool fast = kind == 9 || kind == 10;
+    Code c = make_code(N, K, list ? L : 1, v, frozen, fast ? node_type : nullptr, nullptr, nullptr, 0, nullptr,
+                       nullptr, 0, nullptr, 0);
+    if (N < 2 || (1 << c.n) != N) return -1;
+    FloatDom dom;
+    dom.v = v;
+    dom.nodes = N - 1;
+    if (kind == 11 || kind == 12) {
+        dom.quant = Q_UNIFORM;
+        dom.r_f = r_f;
+        dom.r_g = r_g;
+    } else if (kind == 13 || kind == 14) {
+        dom.quant = Q_LLOYD;
+        dom.bnd = bnd;
+        dom.bnd_off = bnd_off;
+        dom.bnd_len = bnd_len;
+        dom.rec = rec;
+        dom.rec_off = rec_off;
+        dom.rec_len = rec_len;
+    } else if (kind != 0 && kind != 7 && kind != 8 && kind != 9 && kind != 10) {
+        return -3;
+    }
+    if (!list) {
+        SCDec<FloatDom> dec(c, dom, fast);
+        for (int64_t b = 0; b < B; ++b) {
+            int rc = dec.run(llr + b * N, out + b * K);
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    SCLDec<FloatDom> dec(c, dom, fast);
+    dec.pm_init = kind == 10 ? kInf : 1e300;
+    int ob = K;
+    if (kind == 8) {
+        if (A < 1 || crc_n < 1 || A + crc_n > K) return -1;
+        dec.ca.A = A;
+        dec.ca.crc_n = crc_n;
+        dec.ca.nchk = crc_n;
+        dec.ca.p.assign(crc_n + 1, 0);
+        for (int i = 0; i < n_loc; ++i) dec.ca.p[crc_loc[i]] = 1;
+        ob = A;
+    }
+    for (int64_t b = 0; b < B; ++b) {
+        int rc = dec.run(llr + b * N, out + b * ob);
+        if (rc) return rc;
+    }
     return 0;
 }
 

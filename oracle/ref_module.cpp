@@ -14,6 +14,14 @@ void init_FastSCLUTDecoder(py::module &m);
 void init_FastSCLLUTDecoder(py::module &m);
 void init_CASCLLUTDecoder(py::module &m);
 void init_CAFastSCLLUTDecoder(py::module &m);
+void init_SCLDecoder(py::module &m);
+void init_CASCLDecoder(py::module &m);
+void init_FastSCDecoder(py::module &m);
+void init_FastSCLDecoder(py::module &m);
+void init_SCUniformQuantizedDecoder(py::module &m);
+void init_SCLUniformQuantizedDecoder(py::module &m);
+void init_SCLloydQuantizedDecoder(py::module &m);
+void init_SCLLloydQuantizedDecoder(py::module &m);
 
 PYBIND11_MODULE(_refPolarDecoder, m) {
     m.doc() = "reference decoders (oracle build, test-only)";
@@ -24,4 +32,12 @@ PYBIND11_MODULE(_refPolarDecoder, m) {
     init_FastSCLLUTDecoder(m);
     init_CASCLLUTDecoder(m);
     init_CAFastSCLLUTDecoder(m);
+    init_SCLDecoder(m);
+    init_CASCLDecoder(m);
+    init_FastSCDecoder(m);
+    init_FastSCLDecoder(m);
+    init_SCUniformQuantizedDecoder(m);
+    init_SCLUniformQuantizedDecoder(m);
+    init_SCLloydQuantizedDecoder(m);
+    init_SCLLloydQuantizedDecoder(m);
 }

@@ -18,9 +18,12 @@ def pytest_configure(config):
 
 
 def golden_files(pattern="*.npz"):
-    """Decoder fixtures (the LUT-generator fixtures lutgen_*.npz have their own test)."""
+    """Decoder fixtures.  The default pattern gives the LUT and SC decoders'
+    fixtures; the LUT-generator (lutgen_*.npz) and float-domain (float_*.npz)
+    fixtures have their own tests and are returned only when asked for."""
+    own = ("lutgen_", "float_")
     return sorted(p for p in glob.glob(os.path.join(GOLDEN_DIR, pattern))
-                  if pattern.startswith("lutgen") or not os.path.basename(p).startswith("lutgen_"))
+                  if pattern.startswith(own) or not os.path.basename(p).startswith(own))
 
 
 def load_golden(path):
