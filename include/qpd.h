@@ -13,8 +13,16 @@
  *                             SC::SC              src/SCDecoder.cpp:7-12
  *                             CASCLLUT::CASCLLUT  src/CASCLLUTDecoder.cpp:43-62
  *                             CAFastSCLLUT::CAFastSCLLUT src/CAFastSCLLUTDecoder.cpp:43-56
- *                   bound at py_interface/py_{SCLUT,SCLLUT,FastSCLUT,FastSCLLUT,SC,
- *                   CASCLLUT,CAFastSCLLUT}Decoder.cpp
+ *                             SCL::SCL            src/SCLDecoder.cpp:30-36
+ *                             CASCL::CASCL        src/CASCLDecoder.cpp:42-54
+ *                             FastSC::FastSC      src/FastSCDecoder.cpp:13-19
+ *                             FastSCL::FastSCL    src/FastSCLDecoder.cpp:40-47
+ *                             SCUniformQuantizedDecoder  src/SCUniformQuantizedDecoder.cpp:9-18
+ *                             SCLUniformQuantizedDecoder src/SCLUniformQuantizedDecoder.cpp:31-41
+ *                             SCLloydQuantizedDecoder    src/SCLloydQuantizedDecoder.cpp:6-20
+ *                             SCLLloydQuantizedDecoder   src/SCLLloydQuantizedDecoder.cpp:29-44
+ *                   bound at py_interface/py_*.cpp (all 15 classes of
+ *                   _libPolarDecoder.cpp:29-50)
  *   qpd_decode    <- SCLUT::decode   src/SCLUTDecoder.cpp:21-124
  *                    SCLLUT::decode  src/SCLLUTDecoder.cpp:47-253
  *                    FastSCLUT::decode src/FastSCLUT.cpp:27-206
@@ -23,6 +31,14 @@
  *                    CAFastSCLLUT::decode src/CAFastSCLLUTDecoder.cpp:58-454
  *                   (batched: B frames per call instead of one)
  *   qpd_decode_f64 <- SC::decode     src/SCDecoder.cpp:14-89 (float64 LLR input)
+ *                    SCL::decode    src/SCLDecoder.cpp:38-176
+ *                    CASCL::decode  src/CASCLDecoder.cpp:74-249
+ *                    FastSC::decode src/FastSCDecoder.cpp:21-174
+ *                    FastSCL::decode src/FastSCLDecoder.cpp:49-423
+ *                    SC{,L}UniformQuantizedDecoder::decode src/SCUniformQuantizedDecoder.cpp:20-99,
+ *                        src/SCLUniformQuantizedDecoder.cpp:43-184
+ *                    SC{l,L}loydQuantizedDecoder::decode src/SCLloydQuantizedDecoder.cpp:22-101,
+ *                        src/SCLLloydQuantizedDecoder.cpp:46-187
  *   qpd_decode_host / qpd_decode_f64_host: the same from host buffers
  *                   (copy in, decode, copy out, synchronous) -- what a
  *                   per-frame `decode(symbols)` call needs.
@@ -47,7 +63,7 @@
 extern "C" {
 #endif
 
-#define QPD_ABI_VERSION 2
+#define QPD_ABI_VERSION 3
 
 /* Decoder kinds (the reference's class names). */
 enum qpd_kind {
@@ -57,7 +73,16 @@ enum qpd_kind {
     QPD_FASTSC_LUT = 3,  /* FastSCLUTDecoder  (R0/R1/REP/SPC shortcuts)       */
     QPD_FASTSCL_LUT = 4, /* FastSCLLUTDecoder (R0/R1/REP shortcuts; no SPC)   */
     QPD_CASCL_LUT = 5,   /* CASCLLUTDecoder     (SCL-LUT + CRC-aided output)   */
-    QPD_CAFASTSCL_LUT = 6 /* CAFastSCLLUTDecoder (FastSCL-LUT + CRC-aided output) */
+    QPD_CAFASTSCL_LUT = 6, /* CAFastSCLLUTDecoder (FastSCL-LUT + CRC-aided output) */
+    /* float64-LLR decoders (qpd_decode_f64) */
+    QPD_SCL_FLOAT = 7,   /* SCLDecoder        (min-sum list; PM init 1e300)    */
+    QPD_CASCL_FLOAT = 8, /* CASCLDecoder      (SCL + CRC from crc_n/crc_loc)   */
+    QPD_FASTSC_FLOAT = 9,   /* FastSCDecoder  (R0/R1/REP/SPC shortcuts)        */
+    QPD_FASTSCL_FLOAT = 10, /* FastSCLDecoder (R0/R1/REP shortcuts; no SPC)    */
+    QPD_SC_UNIFORM = 11,  /* SCUniformQuantizedDecoder  (Q after every f/g)   */
+    QPD_SCL_UNIFORM = 12, /* SCLUniformQuantizedDecoder                       */
+    QPD_SC_LLOYD = 13,    /* SCLloydQuantizedDecoder    (bisect after f/g)    */
+    QPD_SCL_LLOYD = 14    /* SCLLloydQuantizedDecoder                         */
 };
 
 enum qpd_status {
@@ -65,7 +90,10 @@ enum qpd_status {
     QPD_E_INVALID = -1,     /* bad argument / configuration                  */
     QPD_E_UNSUPPORTED = -2, /* valid for the reference, not supported here   */
     QPD_E_DEVICE = -3,      /* HIP runtime failure                           */
-    QPD_E_INPUT = -4        /* channel symbol outside [0, v) seen on device  */
+    QPD_E_INPUT = -4        /* input the reference cannot decode defined-ly,
+                               seen on device: a channel symbol outside
+                               [0, v); a Lloyd index outside the
+                               reconstruction list; a NaN path metric       */
 };
 
 /*
@@ -84,7 +112,9 @@ typedef struct qpd_config {
     int32_t N;                  /* code length, power of two, 2..65536            */
     int32_t K;                  /* output bits = number of 0 entries in frozen    */
     int32_t L;                  /* list size (SCL kinds), 1..8; ignored otherwise */
-    int32_t v;                  /* symbol alphabet size, 2..256 (LUT kinds)       */
+    int32_t v;                  /* symbol alphabet size, 2..256 (LUT kinds); the
+                                   re-quantizer's v (uniform kinds: M = (v/2 - 0.5) r_f,
+                                   (v/2 - 1) r_g, integer v/2)                    */
     const int32_t *frozen_bits; /* [N], 1 = frozen, 0 = information               */
     const int32_t *node_type;   /* [2N-1] node labels (Fast kinds), else NULL     */
     const uint8_t *lut_f;       /* [lut_f_count][v][v]                            */
@@ -111,6 +141,23 @@ typedef struct qpd_config {
     int32_t crc_n;              /* CRC length, 1..32                              */
     const int32_t *crc_loc;     /* [crc_loc_count] coefficient indices in [0, crc_n] */
     int32_t crc_loc_count;
+    /* QPD_CASCL_FLOAT honours crc_n/crc_loc as given (CASCLDecoder.cpp:49-53)
+     * and compares exactly crc_n bits after the A info bits: requires
+     * 1 <= A, A + crc_n <= K. */
+    /* Uniform kinds: step r per node_posi (decoder_r_f / decoder_r_g). */
+    const double *r_f;          /* [N-1] */
+    const double *r_g;          /* [N-1] */
+    /* Lloyd kinds: table t (0 = f, 1 = g) of node p is
+     * q_bnd[bnd_off[t*(N-1)+p] ... + bnd_len[...]) (boundaries) and
+     * q_rec[rec_off[...] ... + rec_len[...]) (reconstruction values). */
+    const double *q_bnd;
+    int32_t q_bnd_count;
+    const double *q_rec;
+    int32_t q_rec_count;
+    const int32_t *bnd_off;     /* [2*(N-1)] */
+    const int32_t *bnd_len;     /* [2*(N-1)], >= 1 */
+    const int32_t *rec_off;     /* [2*(N-1)] */
+    const int32_t *rec_len;     /* [2*(N-1)], >= 1 */
 } qpd_config;
 
 /* Kernel selection.  AUTO picks FAST when the tables allow it (one table per
@@ -128,15 +175,18 @@ void qpd_destroy(qpd_decoder *dec);
 /* LUT kinds.  d_symbols: device int32 [B][N]; d_out: device uint8 [B][K]
  * ([B][A] for the CRC-aided kinds; qpd_info.out_bits). */
 int qpd_decode(qpd_decoder *dec, const int32_t *d_symbols, int64_t B, uint8_t *d_out, void *stream);
-/* QPD_SC_FLOAT.  d_llr: device float64 [B][N]; d_out: device uint8 [B][K].  */
+/* float64-LLR kinds (QPD_SC_FLOAT, 7..14).  d_llr: device float64 [B][N];
+ * d_out: device uint8 [B][K] ([B][A] for QPD_CASCL_FLOAT). */
 int qpd_decode_f64(qpd_decoder *dec, const double *d_llr, int64_t B, uint8_t *d_out, void *stream);
 
 /* Host-buffer variants (synchronous). */
 int qpd_decode_host(qpd_decoder *dec, const int32_t *h_symbols, int64_t B, uint8_t *h_out);
 int qpd_decode_f64_host(qpd_decoder *dec, const double *h_llr, int64_t B, uint8_t *h_out);
 
-/* Returns QPD_E_INPUT (and clears the flag) if any decode since the last
- * check saw a channel symbol outside [0, v); synchronizes the device. */
+/* Returns QPD_E_INPUT (and clears the flags) if any decode since the last
+ * check saw a channel symbol outside [0, v), a Lloyd bisect index outside
+ * the reconstruction list, or a NaN path metric reaching a list selection
+ * (each undefined behaviour in the reference); synchronizes the device. */
 int qpd_check_input_error(qpd_decoder *dec);
 
 /*

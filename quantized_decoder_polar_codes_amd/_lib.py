@@ -12,8 +12,12 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QPD_LIB") or os.path.join(HERE, "libqpd.so")
 
-QPD_SC_FLOAT, QPD_SC_LUT, QPD_SCL_LUT, QPD_FASTSC_LUT, QPD_FASTSCL_LUT, QPD_CASCL_LUT, QPD_CAFASTSCL_LUT = range(7)
-ABI_VERSION = 2
+(QPD_SC_FLOAT, QPD_SC_LUT, QPD_SCL_LUT, QPD_FASTSC_LUT, QPD_FASTSCL_LUT, QPD_CASCL_LUT, QPD_CAFASTSCL_LUT,
+ QPD_SCL_FLOAT, QPD_CASCL_FLOAT, QPD_FASTSC_FLOAT, QPD_FASTSCL_FLOAT, QPD_SC_UNIFORM, QPD_SCL_UNIFORM, QPD_SC_LLOYD,
+ QPD_SCL_LLOYD) = range(15)
+FLOAT_KINDS = (QPD_SC_FLOAT, QPD_SCL_FLOAT, QPD_CASCL_FLOAT, QPD_FASTSC_FLOAT, QPD_FASTSCL_FLOAT, QPD_SC_UNIFORM,
+               QPD_SCL_UNIFORM, QPD_SC_LLOYD, QPD_SCL_LLOYD)
+ABI_VERSION = 3
 QPD_ENGINE_AUTO, QPD_ENGINE_GENERIC, QPD_ENGINE_FAST = range(3)
 QPD_OK, QPD_E_INVALID, QPD_E_UNSUPPORTED, QPD_E_DEVICE, QPD_E_INPUT = 0, -1, -2, -3, -4
 
@@ -65,6 +69,16 @@ class QpdConfig(ctypes.Structure):
         ("crc_n", _i32),
         ("crc_loc", _P),
         ("crc_loc_count", _i32),
+        ("r_f", _P),
+        ("r_g", _P),
+        ("q_bnd", _P),
+        ("q_bnd_count", _i32),
+        ("q_rec", _P),
+        ("q_rec_count", _i32),
+        ("bnd_off", _P),
+        ("bnd_len", _P),
+        ("rec_off", _P),
+        ("rec_len", _P),
     ]
 
 

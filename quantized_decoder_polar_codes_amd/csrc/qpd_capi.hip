@@ -98,7 +98,8 @@ struct DeviceBuf {
 }  // namespace
 
 struct qpd_decoder {
-    int kind, N, n, K, L, v, device;
+    int kind, N, n, K, L, v, device;  // kind: the kernel family (SC/SCL/FastSC/FastSCL LUT ids)
+    int dom = 0;                      // qpd::Dom symbol domain
     int max_waves;
     int64_t scratch_bytes_per_wave;
     int engine = QPD_ENGINE_GENERIC;
@@ -116,6 +117,7 @@ struct qpd_decoder {
     int num_mops = 0;
     std::vector<Op> ops_host;
     DeviceBuf lut_f, f_base, lut_g, g_base, vcl, ops, info_pos, scratch, err;
+    DeviceBuf r_f, r_g, q_bnd, q_rec, bnd_off, bnd_len, rec_off, rec_len;  // float-domain re-quantizers
     // staging for the host-buffer entry points
     DeviceBuf h_in, h_out;
     size_t h_in_bytes = 0, h_out_bytes = 0;
@@ -136,21 +138,51 @@ int set_device(const qpd_decoder *d) {
     return QPD_OK;
 }
 
-int validate(const qpd_config *c, int *n_out) {
+// Kernel family (SC / SCL / FastSC / FastSCL, as the LUT kind ids) and symbol
+// domain of every public kind; the CRC-aided kinds are their list family
+// plus an output epilogue.
+bool family_of(int kind, int *fam, int *dom) {
+    using namespace qpd;
+    switch (kind) {
+        case QPD_SC_FLOAT: *fam = QPD_SC_LUT; *dom = DOM_FLOAT; return true;
+        case QPD_SC_LUT:
+        case QPD_SCL_LUT:
+        case QPD_FASTSC_LUT:
+        case QPD_FASTSCL_LUT: *fam = kind; *dom = DOM_LUT; return true;
+        case QPD_CASCL_LUT: *fam = QPD_SCL_LUT; *dom = DOM_LUT; return true;
+        case QPD_CAFASTSCL_LUT: *fam = QPD_FASTSCL_LUT; *dom = DOM_LUT; return true;
+        case QPD_SCL_FLOAT:
+        case QPD_CASCL_FLOAT: *fam = QPD_SCL_LUT; *dom = DOM_FLOAT; return true;
+        case QPD_FASTSC_FLOAT: *fam = QPD_FASTSC_LUT; *dom = DOM_FLOAT; return true;
+        case QPD_FASTSCL_FLOAT: *fam = QPD_FASTSCL_LUT; *dom = DOM_FLOAT; return true;
+        case QPD_SC_UNIFORM: *fam = QPD_SC_LUT; *dom = DOM_UNIFORM; return true;
+        case QPD_SCL_UNIFORM: *fam = QPD_SCL_LUT; *dom = DOM_UNIFORM; return true;
+        case QPD_SC_LLOYD: *fam = QPD_SC_LUT; *dom = DOM_LLOYD; return true;
+        case QPD_SCL_LLOYD: *fam = QPD_SCL_LUT; *dom = DOM_LLOYD; return true;
+        default: return false;
+    }
+}
+
+bool is_ca(int kind) { return kind == QPD_CASCL_LUT || kind == QPD_CAFASTSCL_LUT || kind == QPD_CASCL_FLOAT; }
+
+int validate(const qpd_config *c, int *n_out, int *fam_out, int *dom_out) {
     if (!c) return fail(QPD_E_INVALID, "null config");
-    if (c->kind < QPD_SC_FLOAT || c->kind > QPD_CAFASTSCL_LUT) return fail(QPD_E_INVALID, "unknown decoder kind");
-    if (c->kind == QPD_CASCL_LUT || c->kind == QPD_CAFASTSCL_LUT) {
-        // CRC-aided output (CASCLLUTDecoder.cpp:263-302): K - A > crc_n would read
-        // past the reference's check code (UB there), so it is rejected here.
+    int fam = 0, dom = 0;
+    if (!family_of(c->kind, &fam, &dom)) return fail(QPD_E_INVALID, "unknown decoder kind");
+    if (is_ca(c->kind)) {
         if (c->crc_n < 1 || c->crc_n > 32) return fail(QPD_E_INVALID, "crc_n must be in [1, 32]");
-        if (c->A < 1 || c->A > c->K || c->K - c->A > c->crc_n)
+        if (c->kind == QPD_CASCL_FLOAT) {
+            // CASCLDecoder.cpp:218-226 compares crc_n bits after the A info bits:
+            // A + crc_n > K would read past the decoded info bits (UB there).
+            if (c->A < 1 || c->A + c->crc_n > c->K) return fail(QPD_E_INVALID, "CASCLDecoder needs 1 <= A and A + crc_n <= K");
+        } else if (c->A < 1 || c->A > c->K || c->K - c->A > c->crc_n) {
+            // CRC-aided LUT output (CASCLLUTDecoder.cpp:263-302): K - A > crc_n would
+            // read past the reference's check code (UB there), so it is rejected here.
             return fail(QPD_E_INVALID, "CRC-aided kinds need 1 <= A <= K and K - A <= crc_n");
+        }
         if (c->crc_loc_count < 0 || (c->crc_loc_count > 0 && !c->crc_loc)) return fail(QPD_E_INVALID, "bad crc_loc");
         for (int i = 0; i < c->crc_loc_count; ++i)
             if (c->crc_loc[i] < 0 || c->crc_loc[i] > c->crc_n) return fail(QPD_E_INVALID, "crc_loc entry outside [0, crc_n]");
-        qpd_config base = *c;
-        base.kind = c->kind == QPD_CASCL_LUT ? QPD_SCL_LUT : QPD_FASTSCL_LUT;
-        return validate(&base, n_out);
     }
     const int n = ilog2_exact(c->N);
     if (c->N < 2 || n < 0 || n > qpd::kMaxDepth) return fail(QPD_E_INVALID, "N must be a power of two in [2, 65536]");
@@ -163,10 +195,28 @@ int validate(const qpd_config *c, int *n_out) {
     }
     if (zeros != c->K) return fail(QPD_E_INVALID, "K must equal the number of information (0) entries of frozen_bits");
     *n_out = n;
-    if (c->kind == QPD_SC_FLOAT) return QPD_OK;
-    const bool list = c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT;
+    *fam_out = fam;
+    *dom_out = dom;
+    const bool list = fam == QPD_SCL_LUT || fam == QPD_FASTSCL_LUT;
     if (list && (c->L < 1 || c->L > qpd::kMaxL))
         return fail(QPD_E_UNSUPPORTED, "list size L must be in [1, 8] (2L <= 16: libstdc++ insertion-sort regime)");
+    if (fam == QPD_FASTSC_LUT || fam == QPD_FASTSCL_LUT) {
+        if (!c->node_type) return fail(QPD_E_INVALID, "node_type is required for the Fast decoders");
+        if (special_of(fam, c->node_type, 0) >= 0)
+            return fail(QPD_E_UNSUPPORTED, "root node labelled special (undefined behaviour in the reference)");
+    }
+    if (dom == qpd::DOM_UNIFORM && (!c->r_f || !c->r_g)) return fail(QPD_E_INVALID, "uniform kinds need r_f and r_g");
+    if (dom == qpd::DOM_LLOYD) {
+        if (!c->q_bnd || !c->q_rec || !c->bnd_off || !c->bnd_len || !c->rec_off || !c->rec_len)
+            return fail(QPD_E_INVALID, "Lloyd kinds need boundary and reconstruction tables");
+        for (int k = 0; k < 2 * (c->N - 1); ++k) {
+            if (c->bnd_len[k] < 1 || c->bnd_off[k] < 0 || (long)c->bnd_off[k] + c->bnd_len[k] > c->q_bnd_count)
+                return fail(QPD_E_INVALID, "Lloyd boundary list outside q_bnd (or empty)");
+            if (c->rec_len[k] < 1 || c->rec_off[k] < 0 || (long)c->rec_off[k] + c->rec_len[k] > c->q_rec_count)
+                return fail(QPD_E_INVALID, "Lloyd reconstruction list outside q_rec (or empty)");
+        }
+    }
+    if (dom != qpd::DOM_LUT) return QPD_OK;
     if (c->v < 2 || c->v > 256) return fail(QPD_E_INVALID, "alphabet size v must be in [2, 256]");
     if (!c->lut_f || !c->lut_g || !c->f_base || !c->g_base || !c->vcl) return fail(QPD_E_INVALID, "null table pointer");
     if ((c->f_step != 0 && c->f_step != 1) || (c->g_step != 0 && c->g_step != 1))
@@ -187,11 +237,6 @@ int validate(const qpd_config *c, int *n_out) {
         if (c->lut_g[i] >= c->v) return fail(QPD_E_INVALID, "lut_g entry outside [0, v)");
     for (long i = 0; i < (long)n * c->N * c->v; ++i)
         if (!std::isfinite(c->vcl[i])) return fail(QPD_E_INVALID, "vcl rows 0..n-1 must be finite");
-    if (c->kind == QPD_FASTSC_LUT || c->kind == QPD_FASTSCL_LUT) {
-        if (!c->node_type) return fail(QPD_E_INVALID, "node_type is required for the Fast decoders");
-        if (special_of(c->kind, c->node_type, 0) >= 0)
-            return fail(QPD_E_UNSUPPORTED, "root node labelled special (undefined behaviour in the reference)");
-    }
     return QPD_OK;
 }
 
@@ -519,6 +564,47 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     return QPD_OK;
 }
 
+// Generic-engine instantiations generic_decode_kernel<family, domain>: every
+// family in the LUT and plain float domains; the re-quantized domains exist
+// only for SC and SCL (SC{,L}{Uniform,Lloyd}QuantizedDecoder).
+const void *generic_kernel(int fam, int dom) {
+    using namespace qpd;
+#define QPD_GK(K, D) reinterpret_cast<const void *>(&generic_decode_kernel<K, D>)
+#define QPD_GK4(D)                                             \
+    switch (fam) {                                             \
+        case QPD_SC_LUT: return QPD_GK(K_SC_LUT, D);           \
+        case QPD_SCL_LUT: return QPD_GK(K_SCL_LUT, D);         \
+        case QPD_FASTSC_LUT: return QPD_GK(K_FASTSC_LUT, D);   \
+        case QPD_FASTSCL_LUT: return QPD_GK(K_FASTSCL_LUT, D); \
+        default: return nullptr;                               \
+    }
+    switch (dom) {
+        case DOM_LUT: QPD_GK4(DOM_LUT)
+        case DOM_FLOAT: QPD_GK4(DOM_FLOAT)
+        case DOM_UNIFORM:
+            return fam == QPD_SC_LUT ? QPD_GK(K_SC_LUT, DOM_UNIFORM)
+                                     : fam == QPD_SCL_LUT ? QPD_GK(K_SCL_LUT, DOM_UNIFORM) : nullptr;
+        case DOM_LLOYD:
+            return fam == QPD_SC_LUT ? QPD_GK(K_SC_LUT, DOM_LLOYD)
+                                     : fam == QPD_SCL_LUT ? QPD_GK(K_SCL_LUT, DOM_LLOYD) : nullptr;
+        default: return nullptr;
+    }
+#undef QPD_GK4
+#undef QPD_GK
+}
+
+template <class In>
+int launch_generic(qpd_decoder *d, const In *in, int64_t B, uint8_t *out, int grid, hipStream_t st) {
+    const void *kfn = generic_kernel(d->kind, d->dom);
+    if (!kfn) return fail(QPD_E_INVALID, "bad kind");
+    qpd::DevPlan P = d->plan;
+    const In *in_arg = in;
+    void *args[] = {&P, &in_arg, &B, &out};
+    QPD_HIP(hipLaunchKernel(kfn, dim3(grid), dim3(64), args, 0, st));
+    QPD_HIP(hipGetLastError());
+    return QPD_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -530,18 +616,20 @@ const char *qpd_last_error(void) { return g_err.c_str(); }
 int qpd_create(const qpd_config *cfg, qpd_decoder **out) {
     if (!out) return fail(QPD_E_INVALID, "null output handle");
     *out = nullptr;
-    int n = 0;
-    int rc = validate(cfg, &n);
+    int n = 0, fam = 0, dom = 0;
+    int rc = validate(cfg, &n, &fam, &dom);
     if (rc) return rc;
-    // The CRC-aided kinds are their list kind plus an output epilogue.
+    // Every public kind is a kernel family in a symbol domain (family_of); the
+    // CRC-aided kinds add an output epilogue.
     qpd_config cc = *cfg;
-    const bool ca = cfg->kind == QPD_CASCL_LUT || cfg->kind == QPD_CAFASTSCL_LUT;
-    if (ca) cc.kind = cfg->kind == QPD_CASCL_LUT ? QPD_SCL_LUT : QPD_FASTSCL_LUT;
+    const bool ca = is_ca(cfg->kind);
+    cc.kind = fam;
     const qpd_config *c = &cc;
     if (c->device >= 0) QPD_HIP(hipSetDevice(c->device));
 
     qpd_decoder *d = new qpd_decoder();
     d->pub_kind = cfg->kind;
+    d->dom = dom;
     d->out_bits = ca ? cfg->A : cfg->K;
     if (ca) {
         d->ca_A = cfg->A;
@@ -557,19 +645,20 @@ int qpd_create(const qpd_config *cfg, qpd_decoder **out) {
     d->K = c->K;
     const bool list = c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT;
     d->L = list ? c->L : 1;
-    d->v = c->kind == QPD_SC_FLOAT ? 0 : c->v;
+    d->v = (dom == qpd::DOM_LUT || dom == qpd::DOM_UNIFORM) ? c->v : 0;
     d->device = c->device;
 
     Schedule s;
     visit(s, c->kind, c->N, n, c->frozen_bits, (c->kind == QPD_FASTSC_LUT || c->kind == QPD_FASTSCL_LUT) ? c->node_type : nullptr, 0, 0);
     d->ops_host = s.ops;
     {
-        const bool fast_ok = c->kind != QPD_SC_FLOAT && c->f_step == 0 && c->g_step == 0 && c->v <= 16;
+        const bool fast_ok = dom == qpd::DOM_LUT && c->f_step == 0 && c->g_step == 0 && c->v <= 16;
         int want = c->engine;
         if (const char *e = getenv("QPD_ENGINE")) want = atoi(e);
         if (want == QPD_ENGINE_FAST && !fast_ok) {
             delete d;
-            return fail(QPD_E_UNSUPPORTED, "fast engine needs one table per node (f_step = g_step = 0) and v <= 16");
+            return fail(QPD_E_UNSUPPORTED,
+                        "fast engine needs LUT symbols with one table per node (f_step = g_step = 0) and v <= 16");
         }
         d->engine = (want == QPD_ENGINE_GENERIC || !fast_ok) ? QPD_ENGINE_GENERIC : QPD_ENGINE_FAST;
     }
@@ -592,7 +681,7 @@ int qpd_create(const qpd_config *cfg, qpd_decoder **out) {
     for (int dd = 0; dd <= qpd::kMaxDepth; ++dd) P.So[dd] = P.Uo[dd] = 0;
     for (int dd = 1; dd <= n - 1; ++dd) {
         P.So[dd] = r;
-        r += c->kind == QPD_SC_FLOAT ? 2 * (N >> dd) : std::max(1, ((N >> dd) + 3) / 4);
+        r += dom != qpd::DOM_LUT ? 2 * (N >> dd) : std::max(1, ((N >> dd) + 3) / 4);
     }
     for (int dd = 1; dd <= n; ++dd) {
         P.Uo[dd] = r;
@@ -637,7 +726,18 @@ int qpd_create(const qpd_config *cfg, qpd_decoder **out) {
         for (int i : info) mask[i >> 5] |= 1u << (i & 31);
         QPD_TRY(upload(d->info_mask, mask.data(), mask.size()));
     }
-    if (c->kind != QPD_SC_FLOAT) {
+    if (dom == qpd::DOM_UNIFORM) {
+        QPD_TRY(upload(d->r_f, c->r_f, (size_t)N - 1));
+        QPD_TRY(upload(d->r_g, c->r_g, (size_t)N - 1));
+    } else if (dom == qpd::DOM_LLOYD) {
+        QPD_TRY(upload(d->q_bnd, c->q_bnd, (size_t)c->q_bnd_count));
+        QPD_TRY(upload(d->q_rec, c->q_rec, (size_t)c->q_rec_count));
+        QPD_TRY(upload(d->bnd_off, c->bnd_off, 2 * ((size_t)N - 1)));
+        QPD_TRY(upload(d->bnd_len, c->bnd_len, 2 * ((size_t)N - 1)));
+        QPD_TRY(upload(d->rec_off, c->rec_off, 2 * ((size_t)N - 1)));
+        QPD_TRY(upload(d->rec_len, c->rec_len, 2 * ((size_t)N - 1)));
+    }
+    if (dom == qpd::DOM_LUT) {
         const size_t vv = (size_t)c->v * c->v;
         QPD_TRY(upload(d->lut_f, c->lut_f, (size_t)c->lut_f_count * vv));
         QPD_TRY(upload(d->lut_g, c->lut_g, (size_t)c->lut_g_count * 2 * vv));
@@ -670,9 +770,23 @@ int qpd_create(const qpd_config *cfg, qpd_decoder **out) {
     P.info_pos = (const int32_t *)d->info_pos.p;
     P.scratch = (uint32_t *)d->scratch.p;
     P.err = (int32_t *)d->err.p;
+    P.r_f = (const double *)d->r_f.p;
+    P.r_g = (const double *)d->r_g.p;
+    P.q_bnd = (const double *)d->q_bnd.p;
+    P.q_rec = (const double *)d->q_rec.p;
+    P.bnd_off = (const int32_t *)d->bnd_off.p;
+    P.bnd_len = (const int32_t *)d->bnd_len.p;
+    P.rec_off = (const int32_t *)d->rec_off.p;
+    P.rec_len = (const int32_t *)d->rec_len.p;
+    // DOUBLE_INF of each class: 1.0/0.0 for the LUT decoders and FastSCL
+    // (SCLLUTDecoder.h:16, FastSCLDecoder.h:7), 1e300 for the float SCL family
+    // (SCLDecoder.h:8, CASCLDecoder.h:9, SCL{Uniform,Lloyd}QuantizedDecoder.h)
+    P.pm_init = (dom == qpd::DOM_LUT || c->kind == QPD_FASTSCL_LUT) ? __builtin_huge_val() : 1e300;
     P.out_k = d->out_bits;
     P.ca_A = d->ca_A;
     P.crc_n = d->crc_n;
+    // bits compared after the A info bits: K - A (LUT kinds), crc_n (CASCLDecoder)
+    P.ca_chk = cfg->kind == QPD_CASCL_FLOAT ? d->crc_n : d->K - d->ca_A;
     P.crc_q = d->crc_q;
     P.info_mask = (const uint32_t *)d->info_mask.p;
     d->fplan.out_k = d->out_bits;
@@ -707,7 +821,7 @@ int qpd_get_info(const qpd_decoder *d, qpd_info *info) {
 
 int qpd_decode(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_out, void *stream) {
     if (!d) return fail(QPD_E_INVALID, "null decoder");
-    if (d->kind == QPD_SC_FLOAT) return fail(QPD_E_INVALID, "SC float decoder takes float64 LLRs: use qpd_decode_f64");
+    if (d->dom != qpd::DOM_LUT) return fail(QPD_E_INVALID, "this decoder takes float64 LLRs: use qpd_decode_f64");
     if (B < 0) return fail(QPD_E_INVALID, "negative batch");
     if (B == 0) return QPD_OK;
     if (!d_symbols || !d_out) return fail(QPD_E_INVALID, "null buffer");
@@ -735,39 +849,20 @@ int qpd_decode(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_o
         QPD_HIP(hipGetLastError());
         return QPD_OK;
     }
-    switch (d->kind) {
-        case QPD_SC_LUT:
-            hipLaunchKernelGGL(qpd::lut_decode_kernel<qpd::K_SC_LUT>, dim3(grid), dim3(64), 0, st, d->plan, d_symbols, B, d_out);
-            break;
-        case QPD_SCL_LUT:
-            hipLaunchKernelGGL(qpd::lut_decode_kernel<qpd::K_SCL_LUT>, dim3(grid), dim3(64), 0, st, d->plan, d_symbols, B, d_out);
-            break;
-        case QPD_FASTSC_LUT:
-            hipLaunchKernelGGL(qpd::lut_decode_kernel<qpd::K_FASTSC_LUT>, dim3(grid), dim3(64), 0, st, d->plan, d_symbols, B, d_out);
-            break;
-        case QPD_FASTSCL_LUT:
-            hipLaunchKernelGGL(qpd::lut_decode_kernel<qpd::K_FASTSCL_LUT>, dim3(grid), dim3(64), 0, st, d->plan, d_symbols, B, d_out);
-            break;
-        default:
-            return fail(QPD_E_INVALID, "bad kind");
-    }
-    QPD_HIP(hipGetLastError());
-    return QPD_OK;
+    return launch_generic(d, d_symbols, B, d_out, grid, st);
 }
 
 int qpd_decode_f64(qpd_decoder *d, const double *d_llr, int64_t B, uint8_t *d_out, void *stream) {
     if (!d) return fail(QPD_E_INVALID, "null decoder");
-    if (d->kind != QPD_SC_FLOAT) return fail(QPD_E_INVALID, "qpd_decode_f64 is for the SC float decoder");
+    if (d->dom == qpd::DOM_LUT) return fail(QPD_E_INVALID, "LUT decoders take int32 channel symbols: use qpd_decode");
     if (B < 0) return fail(QPD_E_INVALID, "negative batch");
     if (B == 0) return QPD_OK;
     if (!d_llr || !d_out) return fail(QPD_E_INVALID, "null buffer");
     int rc = set_device(d);
     if (rc) return rc;
-    const int64_t groups = (B + 63) / 64;
+    const int64_t groups = (B + d->plan.fpw - 1) / d->plan.fpw;
     const int grid = (int)std::min<int64_t>(groups, d->max_waves);
-    hipLaunchKernelGGL(qpd::sc_float_kernel, dim3(grid), dim3(64), 0, (hipStream_t)stream, d->plan, d_llr, B, d_out);
-    QPD_HIP(hipGetLastError());
-    return QPD_OK;
+    return launch_generic(d, d_llr, B, d_out, grid, (hipStream_t)stream);
 }
 
 int qpd_check_input_error(qpd_decoder *d) {
@@ -779,7 +874,12 @@ int qpd_check_input_error(qpd_decoder *d) {
     QPD_HIP(hipMemcpy(&flag, d->err.p, sizeof(flag), hipMemcpyDeviceToHost));
     if (flag) {
         QPD_HIP(hipMemset(d->err.p, 0, sizeof(int32_t)));
-        return fail(QPD_E_INPUT, "channel symbol outside [0, v) in decoder input");
+        std::string msg;
+        if (flag & qpd::ERR_SYMBOL) msg += "channel symbol outside [0, v) in decoder input; ";
+        if (flag & qpd::ERR_LLOYD) msg += "Lloyd bisect index outside the reconstruction list (reference UB); ";
+        if (flag & qpd::ERR_NAN_PM) msg += "NaN path metric reached the list sort (reference UB); ";
+        msg.resize(msg.size() - 2);
+        return fail(QPD_E_INPUT, msg);
     }
     return QPD_OK;
 }
@@ -820,8 +920,7 @@ int qpd_decode_f64_host(qpd_decoder *d, const double *h_llr, int64_t B, uint8_t 
     QPD_HIP(hipMemcpy(d->h_in.p, h_llr, in_b, hipMemcpyHostToDevice));
     if ((rc = qpd_decode_f64(d, (const double *)d->h_in.p, B, (uint8_t *)d->h_out.p, nullptr))) return rc;
     if (out_b) QPD_HIP(hipMemcpy(h_out, d->h_out.p, out_b, hipMemcpyDeviceToHost));
-    QPD_HIP(hipDeviceSynchronize());
-    return QPD_OK;
+    return qpd_check_input_error(d);
 }
 
 int qpd_mc_frames(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64_t frame0, int64_t B, uint8_t *d_msg,

@@ -27,7 +27,16 @@ constexpr int kMaxDepth = 16;  // N <= 65536
 constexpr int kMaxL = 8;       // 2L <= 16: libstdc++ sorts by insertion (stable)
 constexpr int kMaxM = kMaxL - 1;
 
+// Decoder families of the kernels (the float-domain decoders use the same
+// family ids with a DOM_* symbol domain; K_SC_FLOAT is the C-ABI's kind 0).
 enum Kind : int32_t { K_SC_FLOAT = 0, K_SC_LUT = 1, K_SCL_LUT = 2, K_FASTSC_LUT = 3, K_FASTSCL_LUT = 4 };
+
+// Symbol domains of the generic engine: LUT symbols (int, f/g by tables) or
+// fp64 LLRs (min-sum f/g), optionally re-quantized after every f/g.
+enum Dom : int32_t { DOM_LUT = 0, DOM_FLOAT = 1, DOM_UNIFORM = 2, DOM_LLOYD = 3 };
+
+// Device error flags (DevPlan/FastPlan err word).
+enum ErrFlag : int32_t { ERR_SYMBOL = 1, ERR_LLOYD = 2, ERR_NAN_PM = 4 };
 
 
 
@@ -177,17 +186,20 @@ __device__ __forceinline__ Sel select_survivors8(double kk, double kf, int gl, i
 }
 
 // CRC-aided choice of the output path (CASCLLUTDecoder.cpp:263-290,
-// CAFastSCLLUTDecoder.cpp:333-371): the paths in stable path-metric order
-// (argsort of L <= 8 doubles is libstdc++'s insertion sort, H1); the first
-// whose info bits [0, A) reproduce bits [A, K) under CRC::encoding
-// (utils.cpp:77-92), else the first in that order.  The reference's bit-array
+// CAFastSCLLUTDecoder.cpp:333-371, CASCLDecoder.cpp:202-235): the paths in
+// stable path-metric order (argsort of L <= 8 doubles is libstdc++'s
+// insertion sort, H1); the first whose info bits [0, A) reproduce the `chk`
+// bits [A, A + chk) under CRC::encoding (utils.cpp:77-92), else the first in
+// that order.  chk = K - A for the LUT kinds (CASCLLUTDecoder.cpp:279), crc_n
+// for the float CA-SCL (CASCLDecoder.cpp:223).  The reference's bit-array
 // long division is run as the equivalent MSB-first register: the divisor's
 // leading coefficient only clears the current bit, `crc_q` holds
 // coefficients 1..crc_n.  `word(w)` = this lane's decoded bits 32w..32w+31;
 // `info_mask` = wave-uniform information-position mask words.
 template <class WordFn>
 __device__ __forceinline__ int ca_winner(double pm, int gl, int gbase, int L, int N, const uint32_t *info_mask, int A,
-                                         int K, int crc_n, uint32_t crc_q, WordFn word) {
+                                         int chk, int crc_n, uint32_t crc_q, WordFn word) {
+    const int K = A + chk;
     int rank = 0;
     for (int j = 0; j < L; ++j) {
         const double o = shfld(pm, gbase + j);
@@ -210,7 +222,7 @@ __device__ __forceinline__ int ca_winner(double pm, int gl, int gbase, int L, in
             if (t < A) {
                 const uint32_t fb = bit ^ ((r & top) ? 1u : 0u);
                 r = ((r << 1) & mask) ^ (crc_q & (0u - fb));
-            } else if (t < K) {
+            } else {
                 pass = pass && bit == ((r >> (crc_n - 1 - (t - A))) & 1u);
             }
             ++t;

@@ -1049,7 +1049,7 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QP
             const Mem &M = Mv[s];
             int best = 0;
             if (kList && P.crc_n > 0) {
-                best = ca_winner(stv[s].pm, gl, gbase, L, N, P.info_mask, P.ca_A, P.K, P.crc_n, P.crc_q,
+                best = ca_winner(stv[s].pm, gl, gbase, L, N, P.info_mask, P.ca_A, P.K - P.ca_A, P.crc_n, P.crc_q,
                                  [&](int w) { return M.ld(rl, r0 + w, lane); });
             } else if (kList) {
                 double bpm = shfld(stv[s].pm, gbase);

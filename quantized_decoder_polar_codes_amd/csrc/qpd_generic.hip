@@ -1,4 +1,5 @@
-// qpd_kernels.hip -- gfx950 kernels for the quantized polar LUT decoders.
+// qpd_generic.hip -- generic gfx950 engine: every decoder of the reference,
+// LUT symbols or fp64 LLRs, any table layout.
 //
 // Work mapping: one 64-lane wavefront per workgroup; a frame
 // owns a group of G = pow2 >= L consecutive lanes, one lane per list path, so
@@ -16,11 +17,26 @@
 // std::sort tie order (H1) -- insertion sort (stable) for 2L <= 16 via exact
 // ranks, full introsort replay (stl_sort.hpp) for the R1 argsort.
 //
+// Symbol domains (template parameter DOM, qpd_common.hpp):
+//   DOM_LUT      int symbols (one byte per element in scratch), f/g by the
+//                per-node tables, node LLR = vcl[row][pos][sym] (H3)
+//   DOM_FLOAT    fp64 LLRs (two dwords per element), min-sum f/g
+//                (utils.cpp:26-36), node LLR = the value itself
+//   DOM_UNIFORM  DOM_FLOAT + uniform re-quantization Q after every f/g
+//                (utils.cpp:8-10, q_f/q_g :38-48)
+//   DOM_LLOYD    DOM_FLOAT + Lloyd bisect after every f/g (utils.cpp:12-24,
+//                non_uniform_q_f/g :50-60)
+// The decoder families (KIND) are the reference's SC / SCL / FastSC / FastSCL
+// classes, so every one of its 15 decoders is one (KIND, DOM) instantiation
+// plus the CRC-aided epilogue.
+//
 // Per-lane state lives in a per-wave scratch slab laid out [row][64 lanes]
 // (one dword per lane per row), so a row access by the wave is one fully
 // coalesced 256-B transaction; cross-lane reads stay inside that line.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 #include "qpd_common.hpp"
 #include "stl_sort.hpp"
@@ -33,18 +49,25 @@ struct DevPlan {
     int32_t rows_per_wave;
     int32_t out_k;         // output bits per frame: K, or A (CRC-aided kinds)
     int32_t ca_A, crc_n;   // crc_n > 0: CRC-aided output (ca_winner)
+    int32_t ca_chk;        // bits compared after the A info bits
     uint32_t crc_q;
+    double pm_init;        // initial metric of paths 1..L-1 (DOUBLE_INF of the class)
     const uint32_t *info_mask;  // [N/32] information-position mask
-    // scratch row offsets: S[d] (symbols of the active node at depth d, bytes),
-    // U[d] (partial sums of the finished left child at depth d, bits),
-    // R (right-chain partial sums, own lane), H (R1 hard decisions),
-    // I / Kd (R1 argsort index / key arrays).
+    // scratch row offsets: S[d] (values of the active node at depth d: bytes
+    // for LUT symbols, two rows per element for fp64), U[d] (partial sums of
+    // the finished left child at depth d, bits), R (right-chain partial sums,
+    // own lane), H (R1 hard decisions), I / Kd (R1 argsort index / key arrays).
     int32_t So[kMaxDepth + 1], Uo[kMaxDepth + 1], Ro, Ho, Io, Ko;
     const uint8_t *lut_f;
     const int32_t *f_base;
     const uint8_t *lut_g;
     const int32_t *g_base;
     const double *vcl;
+    // re-quantizers of the float domains (indexed by node_posi; Lloyd table t
+    // = 0 (f) / 1 (g) of node p at offset/length [t*(N-1) + p])
+    const double *r_f, *r_g;
+    const double *q_bnd, *q_rec;
+    const int32_t *bnd_off, *bnd_len, *rec_off, *rec_len;
     const Op *ops;
     const int32_t *info_pos;
     uint32_t *scratch;
@@ -60,18 +83,105 @@ __device__ __forceinline__ double vcl_at(const DevPlan &P, int row, int pos, int
 __device__ __forceinline__ int in_sym(const DevPlan &P, const int32_t *y, int e) {
     int s = y[e];
     if ((unsigned)s >= (unsigned)P.v) {
-        atomicOr(P.err, 1);
+        atomicOr(P.err, ERR_SYMBOL);
         s = 0;
     }
     return s;
 }
 
 
-// Symbol e of the active node at depth d, for the path whose slot is `src`.
-__device__ __forceinline__ int node_sym(const DevPlan &P, uint32_t *wsc, const int32_t *y, int d, int src, int e) {
-    if (d == 0) return in_sym(P, y, e);
-    uint32_t w = row_ptr(wsc, P.So[d] + (e >> 2))[src];
-    return (int)((w >> (8 * (e & 3))) & 255u);
+// Value e of the active node at depth d, for the path whose slot is `src`.
+template <int DOM, class In>
+__device__ __forceinline__ auto node_val(const DevPlan &P, uint32_t *wsc, const In *y, int d, int src, int e) {
+    if constexpr (DOM == DOM_LUT) {
+        if (d == 0) return in_sym(P, y, e);
+        uint32_t w = row_ptr(wsc, P.So[d] + (e >> 2))[src];
+        return (int)((w >> (8 * (e & 3))) & 255u);
+    } else {
+        if (d == 0) return (double)y[e];
+        return ((const double *)row_ptr(wsc, P.So[d] + 2 * e))[src];
+    }
+}
+
+__device__ __forceinline__ void set_fval(const DevPlan &P, uint32_t *wsc, int d, int e, int lane, double x) {
+    ((double *)row_ptr(wsc, P.So[d] + 2 * e))[lane] = x;
+}
+
+
+// ---------------------------------------------------------------------------
+// fp64 f/g of the float domains, written as the reference writes them and with
+// contraction off so that each product and sum rounds exactly as in its
+// scalar C++ (every product involved is by +-1, 0/1 or 0.5, so FMA would not
+// change a result either; this keeps it true by construction).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int sgn(double x) { return x < 0 ? -1 : (x > 0); }  // utils.h:13
+__device__ __forceinline__ double std_min(double a, double b) { return (b < a) ? b : a; }
+
+// Q(x, r, M), utils.cpp:8-10
+__device__ __forceinline__ double q_uniform(double x, double r, double M) {
+#pragma clang fp contract(off)
+    return fabs(x) > M ? (double)sgn(x) * (M - 0.5 * r) : (floor(x / r) + 0.5) * r;
+}
+
+// bisect, utils.cpp:12-24: reconstruct[lo - 1] with lo = the first index whose
+// boundary is not below x (the same probe sequence, so unsorted lists agree
+// too).  lo - 1 outside the reconstruction list reads out of bounds in the
+// reference (UB): flagged, and 0 is used.
+__device__ __forceinline__ double q_lloyd(const DevPlan &P, double x, int t, int posi) {
+    const int k = t * (P.N - 1) + posi;
+    const double *b = P.q_bnd + P.bnd_off[k];
+    int lo = 0, hi = P.bnd_len[k];
+    while (lo < hi) {
+        const int mid = (lo + hi) / 2;
+        if (b[mid] < x)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    if (lo - 1 < 0 || lo - 1 >= P.rec_len[k]) {
+        atomicOr(P.err, ERR_LLOYD);
+        return 0.0;
+    }
+    return P.q_rec[P.rec_off[k] + lo - 1];
+}
+
+template <int DOM>
+__device__ __forceinline__ double fd_f(const DevPlan &P, int posi, double a, double b) {
+#pragma clang fp contract(off)
+    const double x = (double)(sgn(a) * sgn(b)) * std_min(fabs(a), fabs(b));  // utils.cpp:28
+    if constexpr (DOM == DOM_UNIFORM) {
+        const double r = P.r_f[posi];
+        return q_uniform(x, r, ((double)(P.v / 2) - 0.5) * r);  // SCUniformQuantizedDecoder.cpp:55-57
+    } else if constexpr (DOM == DOM_LLOYD) {
+        return q_lloyd(P, x, 0, posi);
+    } else {
+        return x;
+    }
+}
+
+template <int DOM>
+__device__ __forceinline__ double fd_g(const DevPlan &P, int posi, int u, double a, double b) {
+#pragma clang fp contract(off)
+    const double x = (double)(1 - 2 * u) * a + b;  // utils.cpp:34
+    if constexpr (DOM == DOM_UNIFORM) {
+        const double r = P.r_g[posi];
+        return q_uniform(x, r, (double)(P.v / 2 - 1) * r);  // SCUniformQuantizedDecoder.cpp:71-73
+    } else if constexpr (DOM == DOM_LLOYD) {
+        return q_lloyd(P, x, 1, posi);
+    } else {
+        return x;
+    }
+}
+
+
+// LLR of a node element: the LUT domain reads vcl[row][pos][sym] (H3), the
+// float domains hold the LLR itself.
+template <int DOM, class T>
+__device__ __forceinline__ double node_llr(const DevPlan &P, int row, int pos, T s) {
+    if constexpr (DOM == DOM_LUT)
+        return vcl_at(P, row, pos, s);
+    else
+        return s;
 }
 
 
@@ -95,13 +205,25 @@ struct LaneSortSeq {
     __device__ bool less(int a, int b) { return key(a) < key(b); }
 };
 
+// A NaN path metric would reach std::sort (UB in the reference): flag it.
+template <int DOM>
+__device__ __forceinline__ void check_keys(const DevPlan &P, double a, double b) {
+    if constexpr (DOM != DOM_LUT) {
+        if (a != a || b != b) atomicOr(P.err, ERR_NAN_PM);
+    }
+}
+
 // ---------------------------------------------------------------------------
-// LUT decoders (SC-LUT, SCL-LUT, FastSC-LUT, FastSCL-LUT)
+// The decoders.  KIND = family (SC / SCL / FastSC / FastSCL), DOM = domain.
 // ---------------------------------------------------------------------------
-template <int KIND>
-__global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t *__restrict__ in, int64_t B,
-                                                        uint8_t *__restrict__ out) {
+template <int KIND, int DOM>
+__global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
+                                                            const std::conditional_t<DOM == DOM_LUT, int32_t, double>
+                                                                *__restrict__ in,
+                                                            int64_t B, uint8_t *__restrict__ out) {
     constexpr bool kList = (KIND == K_SCL_LUT || KIND == K_FASTSCL_LUT);
+    constexpr bool kLut = DOM == DOM_LUT;
+    using In = std::conditional_t<kLut, int32_t, double>;
     __shared__ int sel[64];
     const int lane = threadIdx.x;
     const int gs = P.gs;
@@ -112,7 +234,6 @@ __global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t
     const int vv = v * v;
     uint32_t *wsc = P.scratch + (size_t)blockIdx.x * P.rows_per_wave * 64;
     const int64_t ngroups = (B + P.fpw - 1) / P.fpw;
-    const double kInf = __builtin_huge_val();
 
     uint64_t self = 0;
     for (int d = 0; d < kMaxDepth; ++d) self |= (uint64_t)gl << (4 * d);
@@ -121,8 +242,8 @@ __global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t
         int64_t frame = grp * P.fpw + lane / gs;
         const bool frame_ok = frame < B;
         if (!frame_ok) frame = B - 1;
-        const int32_t *y = in + frame * (int64_t)N;
-        double pm = (gl == 0) ? 0.0 : kInf;
+        const In *y = in + frame * (int64_t)N;
+        double pm = (gl == 0) ? 0.0 : P.pm_init;
         uint64_t ps = self, pu = self;
 
         for (int oi = 0; oi < P.nops; ++oi) {
@@ -136,26 +257,41 @@ __global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t
                     const int ctemp = N >> (d + 1);
                     const int src = gbase + ptr_get(ps, d);
                     const int usrc = gbase + ptr_get(pu, d + 1);
-                    const uint8_t *T = isg ? P.lut_g : P.lut_f;
-                    const int tsz = isg ? 2 * vv : vv;
-                    const int tb = isg ? P.g_base[posi] : P.f_base[posi];
-                    const int ts = isg ? P.g_step : P.f_step;
-                    const int nw = (ctemp + 3) >> 2;
-                    for (int w = 0; w < nw; ++w) {
-                        uint32_t ub = 0;
-                        if (isg) ub = row_ptr(wsc, P.Uo[d + 1] + ((4 * w) >> 5))[usrc] >> ((4 * w) & 31);
-                        uint32_t res = 0;
-                        const int ne = ctemp < 4 ? ctemp : 4;
-                        for (int i = 0; i < ne; ++i) {
-                            const int e = 4 * w + i;
-                            const int a = node_sym(P, wsc, y, d, src, e);
-                            const int b = node_sym(P, wsc, y, d, src, e + ctemp);
-                            const int u = (ub >> i) & 1;
-                            const size_t t = (size_t)(tb + e * ts);
-                            const uint32_t val = T[t * tsz + u * vv + a * v + b];
-                            res |= val << (8 * i);
+                    if constexpr (kLut) {
+                        const uint8_t *T = isg ? P.lut_g : P.lut_f;
+                        const int tsz = isg ? 2 * vv : vv;
+                        const int tb = isg ? P.g_base[posi] : P.f_base[posi];
+                        const int ts = isg ? P.g_step : P.f_step;
+                        const int nw = (ctemp + 3) >> 2;
+                        for (int w = 0; w < nw; ++w) {
+                            uint32_t ub = 0;
+                            if (isg) ub = row_ptr(wsc, P.Uo[d + 1] + ((4 * w) >> 5))[usrc] >> ((4 * w) & 31);
+                            uint32_t res = 0;
+                            const int ne = ctemp < 4 ? ctemp : 4;
+                            for (int i = 0; i < ne; ++i) {
+                                const int e = 4 * w + i;
+                                const int a = node_val<DOM>(P, wsc, y, d, src, e);
+                                const int b = node_val<DOM>(P, wsc, y, d, src, e + ctemp);
+                                const int u = (ub >> i) & 1;
+                                const size_t t = (size_t)(tb + e * ts);
+                                const uint32_t val = T[t * tsz + u * vv + a * v + b];
+                                res |= val << (8 * i);
+                            }
+                            row_ptr(wsc, P.So[d + 1] + w)[lane] = res;
                         }
-                        row_ptr(wsc, P.So[d + 1] + w)[lane] = res;
+                    } else {
+                        for (int e = 0; e < ctemp; ++e) {
+                            const double a = node_val<DOM>(P, wsc, y, d, src, e);
+                            const double b = node_val<DOM>(P, wsc, y, d, src, e + ctemp);
+                            double r;
+                            if (isg) {
+                                const int u = (row_ptr(wsc, P.Uo[d + 1] + (e >> 5))[usrc] >> (e & 31)) & 1;
+                                r = fd_g<DOM>(P, posi, u, a, b);
+                            } else {
+                                r = fd_f<DOM>(P, posi, a, b);
+                            }
+                            set_fval(P, wsc, d + 1, e, lane, r);
+                        }
                     }
                     ps = ptr_set(ps, d + 1, gl);
                     break;
@@ -168,24 +304,36 @@ __global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t
                     const int src = gbase + ptr_get(ps, d);
                     uint32_t dec = 0;
                     if (!kList && frozen) {
-                        dec = 0;  // SCLUTDecoder.cpp:60-61: frozen leaves skip the LUT
+                        dec = 0;  // SCLUTDecoder.cpp:60-61 / SCDecoder.cpp:25-26: frozen leaves are 0
                     } else {
-                        const int a = node_sym(P, wsc, y, d, src, 0);
-                        const int b = node_sym(P, wsc, y, d, src, 1);
-                        int s;
-                        if (right) {
-                            const int u = row_ptr(wsc, P.Uo[n])[gbase + ptr_get(pu, n)] & 1;
-                            s = P.lut_g[(size_t)P.g_base[posi] * 2 * vv + u * vv + a * v + b];
+                        const auto a = node_val<DOM>(P, wsc, y, d, src, 0);
+                        const auto b = node_val<DOM>(P, wsc, y, d, src, 1);
+                        double dm;
+                        if constexpr (kLut) {
+                            int s;
+                            if (right) {
+                                const int u = row_ptr(wsc, P.Uo[n])[gbase + ptr_get(pu, n)] & 1;
+                                s = P.lut_g[(size_t)P.g_base[posi] * 2 * vv + u * vv + a * v + b];
+                            } else {
+                                s = P.lut_f[(size_t)P.f_base[posi] * vv + a * v + b];
+                            }
+                            dm = vcl_at(P, n - 1, k, s);  // H3: row n-1
                         } else {
-                            s = P.lut_f[(size_t)P.f_base[posi] * vv + a * v + b];
+                            if (right) {
+                                const int u = row_ptr(wsc, P.Uo[n])[gbase + ptr_get(pu, n)] & 1;
+                                dm = fd_g<DOM>(P, posi, u, a, b);
+                            } else {
+                                dm = fd_f<DOM>(P, posi, a, b);
+                            }
                         }
-                        const double dm = vcl_at(P, n - 1, k, s);  // H3: row n-1
                         if (!kList) {
                             dec = dm <= 0;  // H4: SC family `<= 0`
                         } else if (frozen) {
+#pragma clang fp contract(off)
                             pm += fabs(dm) * (double)(dm < 0);  // :100-104
                         } else {
                             const double kf = pm + fabs(dm);
+                            check_keys<DOM>(P, pm, kf);
                             const Sel sl = select_survivors(pm, kf, gl, gbase, L, sel);
                             const int p = gbase + sl.parent;
                             const uint32_t hd = dm < 0;  // H4: SCL family `< 0`
@@ -224,16 +372,22 @@ __global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t
                     if (!to_r) pu = ptr_set(pu, d, gl);
                     break;
                 }
-                default: {  // special nodes, FastSCLUT.cpp:46-107 / FastSCLLUTDecoder.cpp:82-213
+                default: {  // special nodes, FastSCLUT.cpp:46-107 / FastSCLLUTDecoder.cpp:82-213,
+                            // FastSCDecoder.cpp:45-106 / FastSCLDecoder.cpp:122-251
                     const int temp = N >> d;
                     const int src = gbase + ptr_get(ps, d);
                     const bool to_r = (node & 1);
                     const int base_pos = temp * node;
                     const int nwo = (temp + 31) >> 5;
+                    // LLR of element j: vcl row depth-1 (H3) or the value itself
+                    auto lval = [&](int j) {
+                        return node_llr<DOM>(P, d - 1, base_pos + j, node_val<DOM>(P, wsc, y, d, src, j));
+                    };
                     if (op.type == OP_R0) {
                         if (kList) {
+#pragma clang fp contract(off)
                             for (int j = 0; j < temp; ++j) {
-                                const double l = vcl_at(P, d - 1, base_pos + j, node_sym(P, wsc, y, d, src, j));
+                                const double l = lval(j);
                                 pm += (double)(float)(l < 0) * fabs(l);
                             }
                         }
@@ -242,15 +396,17 @@ __global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t
                         uint32_t fill = 0;
                         if (!kList) {
                             double S = 0;
-                            for (int j = 0; j < temp; ++j) S += vcl_at(P, d - 1, base_pos + j, node_sym(P, wsc, y, d, src, j));
+                            for (int j = 0; j < temp; ++j) S += lval(j);
                             fill = S <= 0 ? 0xffffffffu : 0u;
                         } else {
+#pragma clang fp contract(off)
                             double kk = pm, kf = pm;
                             for (int j = 0; j < temp; ++j) {
-                                const double l = vcl_at(P, d - 1, base_pos + j, node_sym(P, wsc, y, d, src, j));
+                                const double l = lval(j);
                                 kk += (double)(l < 0) * fabs(l);
                                 kf += (double)(l >= 0) * fabs(l);
                             }
+                            check_keys<DOM>(P, kk, kf);
                             const Sel sl = select_survivors(kk, kf, gl, gbase, L, sel);
                             const int p = gbase + sl.parent;
                             pm = pick(sl.upper, shfld(kf, p), shfld(kk, p));
@@ -268,7 +424,7 @@ __global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t
                             uint32_t word = 0;
                             for (int i = 0; i < 32 && 32 * w + i < temp; ++i) {
                                 const int j = 32 * w + i;
-                                const double l = vcl_at(P, d - 1, base_pos + j, node_sym(P, wsc, y, d, src, j));
+                                const double l = lval(j);
                                 const uint32_t h = l <= 0;
                                 word |= h << i;
                                 parity ^= h;
@@ -290,8 +446,7 @@ __global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t
                             uint32_t word = 0;
                             for (int i = 0; i < 32 && 32 * w + i < temp; ++i) {
                                 const int j = 32 * w + i;
-                                const double l = vcl_at(P, d - 1, base_pos + j, node_sym(P, wsc, y, d, src, j));
-                                word |= (uint32_t)(l <= 0) << i;
+                                word |= (uint32_t)(lval(j) <= 0) << i;
                             }
                             store_node_word(P, wsc, d, to_r, w, word, lane);
                         }
@@ -302,7 +457,7 @@ __global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t
                             uint32_t word = 0;
                             for (int i = 0; i < 32 && 32 * w + i < temp; ++i) {
                                 const int j = 32 * w + i;
-                                const double l = vcl_at(P, d - 1, base_pos + j, node_sym(P, wsc, y, d, src, j));
+                                const double l = lval(j);
                                 word |= (uint32_t)(l < 0) << i;
                                 ((double *)row_ptr(wsc, P.Ko + 2 * j))[lane] = fabs(l);
                             }
@@ -357,6 +512,7 @@ __global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t
                         for (int layer = 0; layer < kMaxM; ++layer) {
                             if (layer < m) {
                                 const double kf = pm + ms[layer];
+                                check_keys<DOM>(P, pm, kf);
                                 const Sel sl = select_survivors(pm, kf, gl, gbase, L, sel);
                                 const int p = gbase + sl.parent;
                                 const int pos_old = ord[layer];  // H2: own pre-permutation order
@@ -413,7 +569,8 @@ __global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t
         // best path: first minimum of the path metrics (H6, SCLLUTDecoder.cpp:244)
         int best = 0;
         if (kList && P.crc_n > 0) {
-            best = ca_winner(pm, gl, gbase, L, P.N, P.info_mask, P.ca_A, P.K, P.crc_n, P.crc_q,
+            check_keys<DOM>(P, pm, pm);  // the CA epilogue sorts the metrics
+            best = ca_winner(pm, gl, gbase, L, P.N, P.info_mask, P.ca_A, P.ca_chk, P.crc_n, P.crc_q,
                              [&](int w) { return row_ptr(wsc, P.Ro + w)[lane]; });
         } else if (kList) {
             double bpm = shfld(pm, gbase);
@@ -433,119 +590,6 @@ __global__ __launch_bounds__(64) void lut_decode_kernel(DevPlan P, const int32_t
             }
         }
         wave_sync();
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Float SC (min-sum on fp64 LLRs), SCDecoder.cpp:14-89; one lane per frame.
-// Scratch: stage d (1..n) fp64 rows at So[d] (2 dword rows per element),
-// U/R bit rows as in the LUT kernel.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ int sgn(double x) { return x < 0 ? -1 : (x > 0); }
-__device__ __forceinline__ double std_min(double a, double b) { return (b < a) ? b : a; }
-
-__global__ __launch_bounds__(64) void sc_float_kernel(DevPlan P, const double *__restrict__ in, int64_t B,
-                                                      uint8_t *__restrict__ out) {
-    const int lane = threadIdx.x;
-    const int N = P.N, n = P.n;
-    uint32_t *wsc = P.scratch + (size_t)blockIdx.x * P.rows_per_wave * 64;
-    const int64_t ngroups = (B + 63) / 64;
-    for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
-        int64_t frame = grp * 64 + lane;
-        const bool frame_ok = frame < B;
-        if (!frame_ok) frame = B - 1;
-        const double *y = in + frame * (int64_t)N;
-        auto alpha = [&](int d, int e) -> double {
-            if (d == 0) return y[e];
-            return ((double *)row_ptr(wsc, P.So[d] + 2 * e))[lane];
-        };
-        auto set_alpha = [&](int d, int e, double x) { ((double *)row_ptr(wsc, P.So[d] + 2 * e))[lane] = x; };
-        for (int oi = 0; oi < P.nops; ++oi) {
-            const Op op = P.ops[oi];
-            const int d = op.d, node = op.node;
-            switch (op.type) {
-                case OP_F:
-                case OP_G: {
-                    const int ctemp = N >> (d + 1);
-                    for (int j = 0; j < ctemp; ++j) {
-                        const double a = alpha(d, j), b = alpha(d, j + ctemp);
-                        double r;
-                        if (op.type == OP_F) {
-                            r = (double)(sgn(a) * sgn(b)) * std_min(fabs(a), fabs(b));
-                        } else {
-                            const int u = (row_ptr(wsc, P.Uo[d + 1] + (j >> 5))[lane] >> (j & 31)) & 1;
-                            r = (double)(1 - 2 * u) * a + b;
-                        }
-                        set_alpha(d + 1, j, r);
-                    }
-                    break;
-                }
-                case OP_LEAF_L:
-                case OP_LEAF_R: {
-                    const bool right = op.type == OP_LEAF_R;
-                    const double a = alpha(d, 0), b = alpha(d, 1);
-                    double l;
-                    if (right) {
-                        const int u = row_ptr(wsc, P.Uo[n])[lane] & 1;
-                        l = (double)(1 - 2 * u) * a + b;
-                    } else {
-                        l = (double)(sgn(a) * sgn(b)) * std_min(fabs(a), fabs(b));
-                    }
-                    const uint32_t dec = op.aux ? 0u : (uint32_t)(l <= 0);
-                    if (right)
-                        row_ptr(wsc, P.Ro)[lane] = dec;
-                    else
-                        row_ptr(wsc, P.Uo[n])[lane] = dec;
-                    break;
-                }
-                case OP_COMB: {
-                    const int ctemp = N >> (d + 1);
-                    const bool to_r = (d == 0) || (node & 1);
-                    if (ctemp < 32) {
-                        const uint32_t m = (1u << ctemp) - 1u;
-                        const uint32_t ul = row_ptr(wsc, P.Uo[d + 1])[lane] & m;
-                        const uint32_t r = row_ptr(wsc, P.Ro)[lane] & m;
-                        store_node_word(P, wsc, d, to_r, 0, (ul ^ r) | (r << ctemp), lane);
-                    } else {
-                        const int cw = ctemp >> 5;
-                        for (int w = 0; w < cw; ++w) {
-                            const uint32_t ul = row_ptr(wsc, P.Uo[d + 1] + w)[lane];
-                            const uint32_t r = row_ptr(wsc, P.Ro + w)[lane];
-                            store_node_word(P, wsc, d, to_r, cw + w, r, lane);
-                            store_node_word(P, wsc, d, to_r, w, ul ^ r, lane);
-                        }
-                    }
-                    break;
-                }
-                default:
-                    break;
-            }
-        }
-        const int nwr = (N + 31) >> 5;
-        for (int w = 0; w < nwr; ++w) {
-            uint32_t x = row_ptr(wsc, P.Ro + w)[lane];
-            if (N < 32) x &= (1u << N) - 1u;
-            x ^= (x >> 1) & 0x55555555u;
-            x ^= (x >> 2) & 0x33333333u;
-            x ^= (x >> 4) & 0x0f0f0f0fu;
-            x ^= (x >> 8) & 0x00ff00ffu;
-            x ^= (x >> 16) & 0x0000ffffu;
-            row_ptr(wsc, P.Ro + w)[lane] = x;
-        }
-        for (int mw = 1; mw < nwr; mw *= 2)
-            for (int i = 0; i < nwr; i += 2 * mw)
-                for (int j = 0; j < mw; ++j) {
-                    uint32_t *a = &row_ptr(wsc, P.Ro + i + j)[lane];
-                    *a ^= row_ptr(wsc, P.Ro + i + mw + j)[lane];
-                }
-        if (frame_ok) {
-            const uint32_t *rb = row_ptr(wsc, P.Ro);
-            for (int t = 0; t < P.K; ++t) {
-                const int pos = P.info_pos[t];
-                out[frame * P.K + t] = (uint8_t)((rb[(size_t)(pos >> 5) * 64 + lane] >> (pos & 31)) & 1u);
-            }
-        }
-        __syncthreads();
     }
 }
 

@@ -1,10 +1,15 @@
-"""Host-side mirror of the reference's pybind11 decoder classes.
+"""Host-side mirror of the reference's pybind11 decoder classes -- all 15 of
+_libPolarDecoder.cpp:29-50.
 
 Same class names, positional order, keyword names and ``decode`` argument as
 the reference (py_interface/py_SCLUTDecoder.cpp:11-14, py_SCLLUTDecoder.cpp:12-15,
 py_FastSCLUTDecoder.cpp:12-15, py_FastSCLLUTDecoder.cpp:13-16,
-py_SCDecoder.cpp:10-12): ``decode`` takes one frame and returns a new
-``numpy.ndarray`` of dtype uint8 and length K.  Every decode runs on the GPU
+py_SCDecoder.cpp:10-12, py_SCLDecoder.cpp:10-12, py_CASCLDecoder.cpp:10-13,
+py_FastSCDecoder.cpp:11-14, py_FastSCLDecoder.cpp:10-13,
+py_SCUniformDecoder.cpp:10-14, py_SCLUniformQuantizedDecoder.cpp:10-14,
+py_SCLloydQuantizedDecoder.cpp:10-15, py_SCLLloydQuantizedDecoder.cpp:10-15):
+``decode`` takes one frame and returns a new ``numpy.ndarray`` of dtype uint8
+and length K (A for the CRC-aided classes).  Every decode runs on the GPU
 through libqpd.so; there is no CPU path.
 
 Additions (not in the reference): ``decode_batch(x[B, N])`` for throughput
@@ -20,9 +25,12 @@ import numpy as np
 
 from . import _lib
 from .lut import PackedLUT, pack_luts
+from .quant import LloydQuant, UniformQuant, pack_lloyd, pack_uniform
 
 __all__ = ["SCDecoder", "SCLUTDecoder", "SCLLUTDecoder", "FastSCLUTDecoder", "FastSCLLUTDecoder",
-           "CASCLLUTDecoder", "CAFastSCLLUTDecoder"]
+           "CASCLLUTDecoder", "CAFastSCLLUTDecoder", "SCLDecoder", "CASCLDecoder", "FastSCDecoder", "FastSCLDecoder",
+           "SCUniformQuantizedDecoder", "SCLUniformQuantizedDecoder", "SCLloydQuantizedDecoder",
+           "SCLLloydQuantizedDecoder"]
 
 # The CRC the reference CA decoders actually check (CASCLLUTDecoder.h:33-34,
 # CAFastSCLLUTDecoder.h:29-30): CRC-24 with these coefficient indices, whatever
@@ -49,11 +57,14 @@ def _torch():
 
 class _DecoderBase:
     _kind: int = -1
-    _float_input = False
+
+    @property
+    def _float_input(self) -> bool:
+        return self._kind in _lib.FLOAT_KINDS
 
     def __init__(self, N, K, L, frozen_bits, message_bits, node_type, packed: PackedLUT | None, device=None,
                  max_waves: int = 0, engine: str = "auto", A: int | None = None, crc_n: int = 24,
-                 crc_loc=CRC24_LOC):
+                 crc_loc=CRC24_LOC, quant: UniformQuant | LloydQuant | None = None):
         self.N = int(N)
         self.K = int(K)
         self.L = int(L)
@@ -92,8 +103,18 @@ class _DecoderBase:
         cfg.max_waves = int(max_waves)
         cfg.engine = {"auto": _lib.QPD_ENGINE_AUTO, "generic": _lib.QPD_ENGINE_GENERIC,
                       "fast": _lib.QPD_ENGINE_FAST}[engine]
+        self.quant = quant
+        if isinstance(quant, UniformQuant):
+            cfg.v = quant.v
+            cfg.r_f, cfg.r_g = _ptr(quant.r_f), _ptr(quant.r_g)
+        elif isinstance(quant, LloydQuant):
+            cfg.v = quant.v
+            cfg.q_bnd, cfg.q_bnd_count = _ptr(quant.bnd), quant.bnd.size
+            cfg.q_rec, cfg.q_rec_count = _ptr(quant.rec), quant.rec.size
+            cfg.bnd_off, cfg.bnd_len = _ptr(quant.bnd_off), _ptr(quant.bnd_len)
+            cfg.rec_off, cfg.rec_len = _ptr(quant.rec_off), _ptr(quant.rec_len)
         self._crc_loc = np.ascontiguousarray(np.asarray(crc_loc, dtype=np.int32))
-        if self._kind in (_lib.QPD_CASCL_LUT, _lib.QPD_CAFASTSCL_LUT):
+        if self._kind in (_lib.QPD_CASCL_LUT, _lib.QPD_CAFASTSCL_LUT, _lib.QPD_CASCL_FLOAT):
             cfg.A, cfg.crc_n = self.A, int(crc_n)
             cfg.crc_loc, cfg.crc_loc_count = _ptr(self._crc_loc), self._crc_loc.size
         h = ctypes.c_void_p()
@@ -231,13 +252,117 @@ class SCDecoder(_DecoderBase):
     """Float SC, min-sum on float64 LLRs (SCDecoder.cpp:14-89)."""
 
     _kind = _lib.QPD_SC_FLOAT
-    _float_input = True
 
     def __init__(self, N, K, frozen_bits, message_bits, **kw):
         super().__init__(N, K, 1, frozen_bits, message_bits, None, None, **kw)
 
     def decode(self, llr):
         return self._decode_one(llr)
+
+
+class _FloatDecoder(_DecoderBase):
+    def decode(self, llr):
+        return self._decode_one(llr)
+
+
+class SCLDecoder(_FloatDecoder):
+    """Float SCL, min-sum list decoding on float64 LLRs (SCLDecoder.cpp:38-176)."""
+
+    _kind = _lib.QPD_SCL_FLOAT
+
+    def __init__(self, N, K, L, frozen_bits, message_bits, **kw):
+        super().__init__(N, K, L, frozen_bits, message_bits, None, None, **kw)
+
+
+class CASCLDecoder(_FloatDecoder):
+    """CRC-aided float SCL (CASCLDecoder.cpp:74-249; ctor py_CASCLDecoder.cpp:10-12).
+    Unlike the CA-LUT classes it checks the CRC it is given: ``crc_n`` bits with
+    divisor coefficients ``crc_p`` (a list of indices, CASCLDecoder.cpp:49-53).
+    ``decode`` returns the A message bits."""
+
+    _kind = _lib.QPD_CASCL_FLOAT
+
+    def __init__(self, N, K, A, L, frozen_bits, message_bits, crc_n, crc_p, **kw):
+        self.crc_n, self.crc_p = int(crc_n), list(crc_p)
+        super().__init__(N, K, L, frozen_bits, message_bits, None, None, A=A, crc_n=int(crc_n), crc_loc=crc_p, **kw)
+
+
+class FastSCDecoder(_FloatDecoder):
+    """Float Fast-SC with R0/R1/REP/SPC nodes (FastSCDecoder.cpp:21-174)."""
+
+    _kind = _lib.QPD_FASTSC_FLOAT
+
+    def __init__(self, N, K, frozen_bits, message_bits, node_type, **kw):
+        super().__init__(N, K, 1, frozen_bits, message_bits, node_type, None, **kw)
+
+
+class FastSCLDecoder(_FloatDecoder):
+    """Float Fast-SCL with R0/R1/REP nodes, no SPC (FastSCLDecoder.cpp:49-423)."""
+
+    _kind = _lib.QPD_FASTSCL_FLOAT
+
+    def __init__(self, N, K, L, frozen_bits, message_bits, node_type, **kw):
+        super().__init__(N, K, L, frozen_bits, message_bits, node_type, None, **kw)
+
+
+class SCUniformQuantizedDecoder(_FloatDecoder):
+    """SC with uniform re-quantization after every f/g (SCUniformQuantizedDecoder.cpp:20-99)."""
+
+    _kind = _lib.QPD_SC_UNIFORM
+
+    def __init__(self, N, K, frozen_bits, message_bits, decoder_r_f, decoder_r_g, v, **kw):
+        super().__init__(N, K, 1, frozen_bits, message_bits, None, None,
+                         quant=pack_uniform(int(N), decoder_r_f, decoder_r_g, int(v)), **kw)
+
+
+class SCLUniformQuantizedDecoder(_FloatDecoder):
+    """SCL with uniform re-quantization (SCLUniformQuantizedDecoder.cpp:43-184)."""
+
+    _kind = _lib.QPD_SCL_UNIFORM
+
+    def __init__(self, N, K, L, frozen_bits, message_bits, decoder_r_f, decoder_r_g, v, **kw):
+        super().__init__(N, K, L, frozen_bits, message_bits, None, None,
+                         quant=pack_uniform(int(N), decoder_r_f, decoder_r_g, int(v)), **kw)
+
+
+class SCLloydQuantizedDecoder(_FloatDecoder):
+    """SC with Lloyd re-quantization after every f/g (SCLloydQuantizedDecoder.cpp:22-101)."""
+
+    _kind = _lib.QPD_SC_LLOYD
+
+    def __init__(self, N, K, frozen_bits, message_bits, boundaries_f, boundaries_g, reconstruction_f,
+                 reconstruction_g, v, **kw):
+        super().__init__(N, K, 1, frozen_bits, message_bits, None, None,
+                         quant=pack_lloyd(int(N), boundaries_f, boundaries_g, reconstruction_f, reconstruction_g,
+                                          int(v)), **kw)
+
+
+class SCLLloydQuantizedDecoder(_FloatDecoder):
+    """SCL with Lloyd re-quantization (SCLLloydQuantizedDecoder.cpp:46-187)."""
+
+    _kind = _lib.QPD_SCL_LLOYD
+
+    def __init__(self, N, K, L, frozen_bits, message_bits, boundaries_f, boundaries_g, reconstruction_f,
+                 reconstruction_g, v, **kw):
+        super().__init__(N, K, L, frozen_bits, message_bits, None, None,
+                         quant=pack_lloyd(int(N), boundaries_f, boundaries_g, reconstruction_f, reconstruction_g,
+                                          int(v)), **kw)
+
+
+FLOAT_CLASSES = {"SC": SCDecoder, "SCL": SCLDecoder, "CA-SCL": CASCLDecoder, "FastSC": FastSCDecoder,
+                 "FastSCL": FastSCLDecoder, "SC-Uniform": SCUniformQuantizedDecoder,
+                 "SCL-Uniform": SCLUniformQuantizedDecoder, "SC-Lloyd": SCLloydQuantizedDecoder,
+                 "SCL-Lloyd": SCLLloydQuantizedDecoder}
+
+
+def from_quant(kind: str, N: int, K: int, frozen_bits, L: int = 1, node_type=None, quant=None, **kw):
+    """Build a float-domain decoder (kind as oracle.FLOAT_KIND) from packed re-quantizers."""
+    cls = FLOAT_CLASSES[kind]
+    obj = cls.__new__(cls)
+    lst = kind in ("SCL", "CA-SCL", "FastSCL", "SCL-Uniform", "SCL-Lloyd")
+    _DecoderBase.__init__(obj, N, K, L if lst else 1, frozen_bits, 1 - np.asarray(frozen_bits), node_type, None,
+                          quant=quant, **kw)
+    return obj
 
 
 def from_packed(kind: str, packed: PackedLUT, K: int, frozen_bits, L: int = 1, node_type=None, **kw):
