@@ -120,6 +120,26 @@ __device__ __forceinline__ uint32_t lut4(uint32_t table, uint32_t idx) {
     return (bperm(table, idx >> 3) >> ((idx & 7u) << 2)) & 15u;
 }
 
+// x F^{(x)5} inside one 32-bit word (the in-word stages of the re-encode).
+__device__ __forceinline__ uint32_t polar_word(uint32_t x) {
+    x ^= (x >> 1) & 0x55555555u;
+    x ^= (x >> 2) & 0x33333333u;
+    x ^= (x >> 4) & 0x0f0f0f0fu;
+    x ^= (x >> 8) & 0x00ff00ffu;
+    x ^= (x >> 16) & 0x0000ffffu;
+    return x;
+}
+
+// Cross-word butterfly stage of the re-encode on a register row (nwr <= 32 words).
+template <int MW>
+__device__ __forceinline__ void xor_stage(uint32_t (&x)[32], int nwr) {
+#pragma unroll
+    for (int i = 0; i < 32; i += 2 * MW)
+#pragma unroll
+        for (int j = 0; j < MW; ++j)
+            if (i + MW + j < nwr) x[i + j] ^= x[i + MW + j];
+}
+
 __device__ __forceinline__ int pfield(uint64_t p, int sh) { return (int)((p >> sh) & 15u); }
 __device__ __forceinline__ uint64_t pset(uint64_t p, int sh, int gl) {
     return (p & ~(15ull << sh)) | ((uint64_t)gl << sh);
@@ -1018,32 +1038,37 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QP
         const uint64_t stamp_t2 = __builtin_amdgcn_s_memtime();
 #endif
 
-        // Root partial sums -> u = x F^{(x)n} (FastSCLUT.cpp:186-198), R[0] rows.
+        // Root partial sums -> u = x F^{(x)n} (FastSCLUT.cpp:186-198), R[0] rows;
+        // output u[info] of the winning path (SCLLUTDecoder.cpp:244-252).
         const int lane = threadIdx.x;
         const int gl = lane & (gs - 1);
         const int gbase = lane & ~(gs - 1);
         const bool rl = P.R0_lds;
         const int r0 = P.R0_row;
         const int nwr = (N + 31) >> 5;
+        const bool dword_out = (P.out_k & 3) == 0 && ((uintptr_t)out & 3) == 0;
+        // Split tail (list decoders without CRC): the winner follows from the
+        // path metrics alone, so only its root row is re-encoded, spread over
+        // the frame's gs lanes (wpl words each; the cross-lane butterfly stages
+        // by shuffles) and staged in this set's LDS rows for the output gather.
+        const int wpl = nwr / gs;
+        const bool split = kList && P.crc_n == 0 && nwr >= gs && wpl <= 8 && wpl <= P.lds_rows;
+        if (!split) {  // every path re-encodes its own row (CRC-aided: each path's CRC is checked)
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            const Mem &M = Mv[s];
-            for (int w = 0; w < nwr; ++w) {
-                uint32_t x = M.ld(rl, r0 + w, lane);
-                if (N < 32) x &= (1u << N) - 1u;
-                x ^= (x >> 1) & 0x55555555u;
-                x ^= (x >> 2) & 0x33333333u;
-                x ^= (x >> 4) & 0x0f0f0f0fu;
-                x ^= (x >> 8) & 0x00ff00ffu;
-                x ^= (x >> 16) & 0x0000ffffu;
-                M.st(rl, r0 + w, lane, x);
+            for (int s = 0; s < NS; ++s) {
+                const Mem &M = Mv[s];
+                for (int w = 0; w < nwr; ++w) {
+                    uint32_t x = M.ld(rl, r0 + w, lane);
+                    if (N < 32) x &= (1u << N) - 1u;
+                    M.st(rl, r0 + w, lane, polar_word(x));
+                }
+                for (int mw = 1; mw < nwr; mw *= 2)
+                    for (int i = 0; i < nwr; i += 2 * mw)
+                        for (int j = 0; j < mw; ++j)
+                            M.st(rl, r0 + i + j, lane, M.ld(rl, r0 + i + j, lane) ^ M.ld(rl, r0 + i + mw + j, lane));
             }
-            for (int mw = 1; mw < nwr; mw *= 2)
-                for (int i = 0; i < nwr; i += 2 * mw)
-                    for (int j = 0; j < mw; ++j)
-                        M.st(rl, r0 + i + j, lane, M.ld(rl, r0 + i + j, lane) ^ M.ld(rl, r0 + i + mw + j, lane));
+            wave_sync();
         }
-        wave_sync();
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             const Mem &M = Mv[s];
@@ -1055,19 +1080,66 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QP
                 double bpm = shfld(stv[s].pm, gbase);
                 for (int j = 1; j < L; ++j) {
                     const double pj = shfld(stv[s].pm, gbase + j);
-                    if (pj < bpm) {
+                    if (pj < bpm) {  // first minimum (H6)
                         bpm = pj;
                         best = j;
                     }
                 }
             }
+            const int src = gbase + best;
+            const int wsh = __builtin_ctz(wpl > 0 ? wpl : 1);
+            if (split) {
+                uint32_t x[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) x[k] = k < wpl ? polar_word(M.ld(rl, r0 + gl * wpl + k, src)) : 0u;
+#pragma unroll
+                for (int mw = 1; mw < 8; mw *= 2)  // word stages inside the lane
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        if (!(k & mw) && k + mw < wpl) x[k] ^= x[k + mw];
+                for (int lm = 1; lm < gs; lm <<= 1)  // word stages across the frame's lanes
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        if (k < wpl) {
+                            const uint32_t o = (uint32_t)__shfl((int)x[k], lane ^ lm);
+                            if (!(gl & lm)) x[k] ^= o;
+                        }
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if (k < wpl) M.lds[k * 64 + lane] = x[k];  // word gl*wpl + k at row k, column lane
+                wave_sync();
+            }
             const int64_t frame = (task * NS + s) * fpw + lane / gs;
             if (frame < B) {
-                for (int t = gl; t < P.out_k; t += gs) {
-                    const int pos = P.info_pos[t];
-                    out[frame * P.out_k + t] = (uint8_t)((M.ld(rl, r0 + (pos >> 5), gbase + best) >> (pos & 31)) & 1u);
+                auto bit = [&](int pos) {
+                    const int w = pos >> 5;
+                    const uint32_t x = split ? M.lds[(w & (wpl - 1)) * 64 + gbase + (w >> wsh)] : M.ld(rl, r0 + w, src);
+                    return (x >> (pos & 31)) & 1u;
+                };
+                if (dword_out) {
+                    // Four output bytes per store; 4 stores' loads issued together.
+                    uint32_t *o32 = (uint32_t *)(out + frame * P.out_k);
+                    const int nc = P.out_k >> 2;
+                    for (int c0 = gl; c0 < nc; c0 += 4 * gs) {
+                        uint32_t wv[4];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const int c = c0 + k * gs;
+                            wv[k] = 0;
+                            if (c < nc) {
+                                const int4 pp = *(const int4 *)(P.info_pos + 4 * c);
+                                wv[k] = bit(pp.x) | (bit(pp.y) << 8) | (bit(pp.z) << 16) | (bit(pp.w) << 24);
+                            }
+                        }
+#pragma unroll
+                        for (int k = 0; k < 4; ++k)
+                            if (c0 + k * gs < nc) o32[c0 + k * gs] = wv[k];
+                    }
+                } else {
+                    for (int t = gl; t < P.out_k; t += gs) out[frame * P.out_k + t] = (uint8_t)bit(P.info_pos[t]);
                 }
             }
+            if (split) wave_sync();  // the LDS rows are reused by the next set / task
         }
         wave_sync();
 #ifdef QPD_STAMPS
