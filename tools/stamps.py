@@ -40,7 +40,11 @@ print(f"total stamped wave-cycles per task {tot / tasks:,.0f}")
 for c in range(32):
     if cnt[c] == 0:
         continue
-    nm = "TAIL" if c == 31 else ({24: "R1<=8", 25: "R1 9-16", 26: "R1>16"}[c] if 24 <= c <= 26 else
+    if os.environ.get("STAMPS_DEPTH"):
+        nm = "TAIL" if c == 31 else (["F", "G", "COMB"][c // 8] + f" d{c % 8}" if c < 24 else
+                                     {24: "BOT3", 25: "LEAF", 26: "R0", 27: "R1", 28: "REP", 29: "SPC"}[c])
+    else:
+        nm = "TAIL" if c == 31 else ({24: "R1<=8", 25: "R1 9-16", 26: "R1>16"}[c] if 24 <= c <= 26 else
                                   names[c // 2] + ("/sync" if c % 2 else ""))
     print(f"  {nm:12s} ops/task {cnt[c] / tasks:8.1f}  cyc/op {acc[c] / cnt[c]:9.0f}  cyc/task {acc[c] / tasks:11,.0f}  "
           f"{100 * acc[c] / tot:5.1f}%")
