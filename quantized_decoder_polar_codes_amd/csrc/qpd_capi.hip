@@ -111,6 +111,10 @@ struct qpd_decoder {
     DeviceBuf info_mask;
     int sets = 1;  // fast engine: frame sets per wave (lut_fast_kernel NS)
     bool l8 = false;  // fast engine: list decoder with L = 8 (select_survivors8)
+    bool pre = false;         // fast engine pre-mode: root_pre_kernel, then the decode on its rows
+    int64_t pre_chunk = 0;    // frames per pre-pass chunk
+    int64_t pre_cap = 0;      // frames pre_buf holds
+    DeviceBuf pre_buf;
     DevPlan plan{};
     qpd::FastPlan fplan{};
     DeviceBuf f_tab, g_tab, fscratch, mops, r1_rank;
@@ -254,8 +258,19 @@ struct FastLayout {
     // depth d (which replaces its whole subtree) runs.
     int lds_base[qpd::kMaxDepth + 2] = {};  // first LDS row of depth dd (dd >= D)
     int lds_end = 0;                        // rows incl. the selection scratch
+    bool pre = false;    // root pre-pass (root_pre_kernel): MF_PRE / MF_GSEL ops at the root
+    bool bfuse = false;  // BOT3 children of depth n-4 nodes fold in the parent's F / G / COMB
     bool lds(int dd) const { return dd >= D; }
 };
+
+// A plain height-3 subtree under (d = n-3, node): one BOT3 op.
+bool bot3_plain(int kind, const int32_t *node_type, int n, int d, int node) {
+    if (n < 3 || d != n - 3) return false;
+    for (int dd = d; dd < n; ++dd)
+        for (int k = 0; k < (1 << (dd - d)); ++k)
+            if (special_of(kind, node_type, (1 << dd) + (node << (dd - d)) + k - 1) >= 0) return false;
+    return true;
+}
 
 // R1 argsort keys of the fast engine (FastSCL, node size <= 32): for element j
 // and symbol s of the node, (rank of |vcl[d-1][pos_j][s]| among all the node's
@@ -287,6 +302,8 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
         m.sh_src = 4 * d;
         if (d == 0)
             m.flags |= MF_CHAN;
+        else if (Ly.pre && d == 1 && node == 0)
+            m.flags |= MF_PRE;  // f(y) words at the start of the frame's pre-pass row (src_row 0)
         else {
             m.src_row = Ly.S[d];
             if (Ly.lds(d)) m.flags |= MF_SRC_LDS;
@@ -320,11 +337,7 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
         return;
     }
     if (n >= 3 && d == n - 3) {
-        bool plain = true;
-        for (int dd = d; dd < n; ++dd)
-            for (int k = 0; k < (1 << (dd - d)); ++k)
-                plain = plain && special_of(kind, node_type, (1 << dd) + (node << (dd - d)) + k - 1) < 0;
-        if (plain) {
+        if (bot3_plain(kind, node_type, n, d, node)) {
             MOp m = base(OP_BOT3);
             for (int j = 0; j < 8; ++j) m.cnt |= (frozen[8 * node + j] == 1) << j;
             m.tab = posi;
@@ -335,6 +348,11 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
         }
     }
     if (d + 1 < n) {
+        // Both children plain BOT3 subtrees of a depth n-4 node (d >= 2: S[d] is
+        // a slab/LDS row): the left BOT3 takes this node's f, the right one its g
+        // and then this node's combine -- no F / G / COMB ops, no S[n-3] rows.
+        const bool fuse = Ly.bfuse && d == n - 4 && d >= 2 && bot3_plain(kind, node_type, n, d + 1, 2 * node) &&
+                          bot3_plain(kind, node_type, n, d + 1, 2 * node + 1);
         for (int side = 0; side < 2; ++side) {
             MOp m = base(side ? OP_G : OP_F);
             m.cnt = N >> (d + 1);
@@ -349,9 +367,30 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
             } else {
                 m.tab = posi * 32;
             }
-            out.push_back(m);
+            if (Ly.pre && d == 0) {  // root in pre-mode: f(y) comes from the pre-pass row, g(y, u) by selects
+                m.flags = (m.flags & ~MF_CHAN) | MF_PRE | MF_GSEL;
+                m.src_row = N >> 4;  // g(y, 0) words; g(y, 1) follow
+            }
+            if (fuse) {
+                const size_t at = out.size();
+                fast_ops(out, Ly, kind, N, n, v, frozen, node_type, vcl, r1tab, d + 1, 2 * node + side);
+                MOp &b = out[at];  // the child's BOT3
+                b.flags = (b.flags & ~MF_SRC_LDS) | (m.flags & MF_SRC_LDS) | MF_BFG;
+                b.src_row = m.src_row;
+                b.sh_src = m.sh_src;
+                b.tab2 = m.tab;
+                if (side) {
+                    b.flags = (b.flags & ~(MF_DST_LDS | MF_TO_R)) | MF_BG | MF_BCOMB | (m.flags & MF_U_LDS);
+                    b.u_row = m.u_row;  // U[n-3]: g's u bits, then the left half of the combine
+                    b.sh_u = m.sh_u;
+                    finish_node(b);  // this node's destination
+                }
+                continue;
+            }
+            if (!(Ly.pre && d == 0 && side == 0)) out.push_back(m);
             fast_ops(out, Ly, kind, N, n, v, frozen, node_type, vcl, r1tab, d + 1, 2 * node + side);
         }
+        if (fuse) return;
     } else {
         for (int side = 0; side < 2; ++side) {
             const int k = 2 * node + side;
@@ -389,20 +428,15 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
 // an op that reads global rows through a pointer when some global write
 // precedes a fork since the last drain; by then the stores have long
 // completed and the drain costs almost nothing.  Single-path kinds (SC, Fast
-// SC) never read another lane's rows.
+// SC) never read another lane's rows.  A BOT3 with the parent's combine
+// folded in (MF_BCOMB) reads U[n-3] through a pointer AFTER its own forks, so
+// any global write before it is drained at its start.
 void place_syncs(std::vector<qpd::MOp> &ops, bool list) {
     using namespace qpd;
     bool dirty = false, exposed = false;
     for (MOp &m : ops) {
         m.flags &= ~MF_SYNC;
         if (!list) continue;
-        const bool src_glb = !(m.flags & (MF_SRC_LDS | MF_CHAN));
-        const bool u_glb = (m.type == OP_G || m.type == OP_COMB || m.type == OP_LEAF_R) && !(m.flags & MF_U_LDS);
-        if (exposed && (src_glb || u_glb)) {
-            m.flags |= MF_SYNC;
-            exposed = dirty = false;
-        }
-        if (!(m.flags & MF_DST_LDS)) dirty = true;
         bool forks = false;
         switch (m.type) {
             case OP_BOT3: forks = m.cnt != 0xff; break;
@@ -412,6 +446,16 @@ void place_syncs(std::vector<qpd::MOp> &ops, bool list) {
             case OP_R1: forks = true; break;
             default: break;
         }
+        const bool src_glb = !(m.flags & (MF_SRC_LDS | MF_CHAN | MF_PRE));
+        const bool u_glb = (m.type == OP_G || m.type == OP_COMB || m.type == OP_LEAF_R ||
+                            (m.type == OP_BOT3 && (m.flags & (MF_BG | MF_BCOMB)))) &&
+                           !(m.flags & MF_U_LDS);
+        const bool late_u = m.type == OP_BOT3 && (m.flags & MF_BCOMB) && !(m.flags & MF_U_LDS) && forks;
+        if ((exposed && (src_glb || u_glb)) || (late_u && dirty)) {
+            m.flags |= MF_SYNC;
+            exposed = dirty = false;
+        }
+        if (!(m.flags & MF_DST_LDS)) dirty = true;
         if (forks && dirty) exposed = true;
     }
 }
@@ -503,8 +547,14 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     d->lds_bytes = NS * (qpd::kSelInts * 4 + rl * 256);
     std::vector<qpd::MOp> mops;
     std::vector<uint16_t> r1tab;
-    fast_ops(mops, Ly, c->kind, N, n, v, c->frozen_bits,
-             (c->kind == QPD_FASTSC_LUT || c->kind == QPD_FASTSCL_LUT) ? c->node_type : nullptr, c->vcl, r1tab, 0, 0);
+    const int32_t *nt_fast = (c->kind == QPD_FASTSC_LUT || c->kind == QPD_FASTSCL_LUT) ? c->node_type : nullptr;
+    // pre-mode: S[1] is whole words (N >= 16) and the root's left child a plain node
+    Ly.pre = n >= 4 && special_of(c->kind, nt_fast, 1) < 0 && !getenv("QPD_NO_PRE");
+    Ly.bfuse = !getenv("QPD_NO_BFUSE");
+    d->pre = Ly.pre;
+    d->pre_chunk = std::max<int64_t>(1, ((int64_t)256 << 20) / N);  // pre-pass rows: N bytes per frame, <= 256 MB
+    if (const char *e = getenv("QPD_PRE_CHUNK")) d->pre_chunk = std::max<int64_t>(1, atoll(e));
+    fast_ops(mops, Ly, c->kind, N, n, v, c->frozen_bits, nt_fast, c->vcl, r1tab, 0, 0);
     if (r1tab.empty()) r1tab.push_back(0);
     {
         int rc = upload(d->r1_rank, r1tab.data(), r1tab.size());
@@ -832,21 +882,50 @@ int qpd_decode(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_o
     hipStream_t st = (hipStream_t)stream;
     if (d->engine == QPD_ENGINE_FAST) {
         const int64_t tw = (int64_t)d->fplan.fpw * d->sets;  // frames per wave task
-        const int64_t fgroups = (B + tw - 1) / tw;
-        int fgrid = (int)std::min<int64_t>(fgroups, d->max_waves);
-        // even out the rounds of the grid-stride loop (no partial last round)
-        const int64_t rounds = (fgroups + fgrid - 1) / fgrid;
-        fgrid = (int)((fgroups + rounds - 1) / rounds);
         const size_t lds = (size_t)d->lds_bytes;
         qpd::FastPlan fp = d->fplan;
         fp.in_vec = ((uintptr_t)d_symbols & 15u) == 0 && (fp.N & 3) == 0;
         const void *kfn = fast_kernel(d->kind, d->sets, d->l8);
         if (!kfn) return fail(QPD_E_INVALID, "bad kind");
-        const int32_t *in_arg = d_symbols;
-        const qpd::MOp *ops_arg = fp.ops;
-        void *args[] = {&fp, &in_arg, &B, &d_out, &ops_arg};
-        QPD_HIP(hipLaunchKernel(kfn, dim3(fgrid), dim3(64), args, lds, st));
-        QPD_HIP(hipGetLastError());
+        auto decode = [&](const int32_t *in_arg, int64_t Bc, uint8_t *out_arg) -> int {
+            const int64_t fgroups = (Bc + tw - 1) / tw;
+            int fgrid = (int)std::min<int64_t>(fgroups, d->max_waves);
+            // even out the rounds of the grid-stride loop (no partial last round)
+            const int64_t rounds = (fgroups + fgrid - 1) / fgrid;
+            fgrid = (int)((fgroups + rounds - 1) / rounds);
+            const qpd::MOp *ops_arg = fp.ops;
+            void *args[] = {&fp, &in_arg, &Bc, &out_arg, &ops_arg};
+            QPD_HIP(hipLaunchKernel(kfn, dim3(fgrid), dim3(64), args, lds, st));
+            QPD_HIP(hipGetLastError());
+            return QPD_OK;
+        };
+        if (!d->pre) {
+            fp.in_shift = fp.n;
+            return decode(d_symbols, B, d_out);
+        }
+        // pre-mode: root pre-pass, then the decode on its rows, chunk by chunk
+        const int64_t chunk = std::min<int64_t>(B, d->pre_chunk);
+        if (d->pre_cap < chunk) {
+            if (d->pre_buf.p) QPD_HIP(hipFree(d->pre_buf.p));
+            d->pre_buf.p = nullptr;
+            d->pre_cap = 0;
+            QPD_HIP(hipMalloc(&d->pre_buf.p, (size_t)chunk * (size_t)fp.N));  // N/4 words per frame
+            d->pre_cap = chunk;
+        }
+        uint32_t *pre = (uint32_t *)d->pre_buf.p;
+        for (int64_t f0 = 0; f0 < B; f0 += chunk) {
+            int64_t Bc = std::min<int64_t>(chunk, B - f0);
+            const int32_t *sym = d_symbols + f0 * fp.N;
+            fp.in_shift = fp.n;
+            const int pgrid = (int)std::min<int64_t>(((Bc << (fp.n - 4)) + 255) / 256, 8192);
+            void *pargs[] = {&fp, &sym, &Bc, &pre};
+            QPD_HIP(hipLaunchKernel(reinterpret_cast<const void *>(&qpd::root_pre_kernel), dim3(pgrid), dim3(256), pargs,
+                                    0, st));
+            QPD_HIP(hipGetLastError());
+            fp.in_shift = fp.n - 2;
+            const int rc = decode((const int32_t *)pre, Bc, d_out + f0 * fp.out_k);
+            if (rc) return rc;
+        }
         return QPD_OK;
     }
     return launch_generic(d, d_symbols, B, d_out, grid, st);

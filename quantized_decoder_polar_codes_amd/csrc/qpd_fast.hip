@@ -41,6 +41,12 @@ enum MopFlag : int32_t {
     MF_R_LDS = 32,    // R rows read by the op (COMB) in LDS
     MF_CHAN = 64,     // S[d] is the channel input (d == 0)
     MF_R1_LDS = 128,  // R1 (> 16 elements): argsort in the free LDS tail starting at row u_row
+    MF_PRE = 256,     // S[1] of the root's left child / the root g inputs: words of the frame's
+                      // pre-pass row (root_pre_kernel), read without a slot pointer
+    MF_GSEL = 512,    // root g in pre-mode: nibble select between g(y, 0) and g(y, 1) by u
+    MF_BFG = 1024,    // BOT3 whose 8 input symbols are f (or g, MF_BG) of its depth n-4 parent's 16:
+    MF_BG = 2048,     //   the parent's F / G op folded in (src = S[n-4], table at tab2, U[n-3] at u_row)
+    MF_BCOMB = 4096,  // right BOT3 that also runs its parent's combine (dst = U/R[n-4])
 };
 
 struct MOp {
@@ -55,12 +61,15 @@ struct MOp {
     int32_t sh_dst;   // F/G: 4*(d+1) (ps); COMB/special/BOT3 left child: 4*d (pu); LEAF_L: 4*n (pu)
     int32_t tab;      // F/LEAF_L: posi*32; G/LEAF_R: posi*64; BOT3: posi of the subtree root; R1: r1_rank offset
     int32_t vrow;     // LEAF: ((n-1)*N + k)*v; special: (d-1)*N + temp*node; BOT3: ((n-1)*N + 8*node)*v
-    int32_t pad0, pad1;
+    int32_t tab2;     // MF_BFG: the parent's table (f: posi*32, g: posi*64)
+    int32_t pad1;
 };
 
 struct FastPlan {
     int32_t N, n, K, L, v, gs, fpw, nops, max_r1;
     int32_t in_vec;               // per launch: input rows are 16-byte aligned
+    int32_t in_shift;             // per launch: log2 int32 words per frame row of `in` (n: channel
+                                  // symbols; n - 2: pre-pass rows, root_pre_kernel)
     int32_t out_k;                // output bits per frame: K, or A (CRC-aided kinds)
     int32_t ca_A, crc_n;          // crc_n > 0: CRC-aided output (ca_winner)
     uint32_t crc_q;
@@ -181,6 +190,7 @@ __device__ __forceinline__ uint32_t chan_word8(const int32_t *y, int e0, bool ve
 // Word w (8 symbols) of S[d] of the path whose slot is `src`.
 __device__ __forceinline__ uint32_t sym_word(const FastPlan &P, const Mem &M, const MOp &op, const int32_t *y, int src,
                                              int w, int cnt = 8) {
+    if (op.flags & MF_PRE) return ((const uint32_t *)y)[op.src_row + w];  // N >= 16: whole words
     if (op.flags & MF_CHAN) return cnt == 8 ? chan_word8(y, 8 * w, P.in_vec, P.v, P.err) : chan_word(y, 8 * w, cnt, P.v, P.err);
     return M.ld(op.flags & MF_SRC_LDS, op.src_row + w, src);
 }
@@ -286,6 +296,48 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
     }
 }
 
+// Bit i of b (i < 8) -> nibble i all ones.
+__device__ __forceinline__ uint32_t nib_mask(uint32_t b) {
+    b &= 0xFFu;
+    b = (b | (b << 12)) & 0x000F000Fu;
+    b = (b | (b << 6)) & 0x03030303u;
+    b = (b | (b << 3)) & 0x11111111u;
+    return b * 15u;
+}
+
+// Root g in pre-mode (MF_GSEL; SCLLUTDecoder.cpp:157-164 at depth 0): the
+// pre-pass row holds g(y, 0) and g(y, 1) of every root position, so the
+// path's symbols are a nibble select by its left-half partial sums u.
+template <int NS>
+__device__ __forceinline__ void gsel_op(const Mem (&M)[NS], const MOp &op, const int32_t *const (&y)[NS],
+                                        const int (&usrc)[NS], int lane) {
+    const int nwo = op.cnt >> 3;  // 1, 2, 4 or a multiple of 8
+    const bool dl = op.flags & MF_DST_LDS, ul = op.flags & MF_U_LDS;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const uint32_t *g = (const uint32_t *)y[s] + op.src_row;  // g(y, 0) words; g(y, 1) at + nwo
+        for (int w0 = 0; w0 < nwo; w0 += 8) {
+            uint32_t g0[8], g1[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                g0[k] = g1[k] = 0u;
+                if (k == 0 || w0 + k < nwo) {
+                    g0[k] = g[w0 + k];
+                    g1[k] = g[nwo + w0 + k];
+                }
+            }
+            const uint32_t u0 = M[s].ld(ul, op.u_row + (w0 >> 2), usrc[s]);
+            const uint32_t u1 = nwo - w0 > 4 ? M[s].ld(ul, op.u_row + (w0 >> 2) + 1, usrc[s]) : 0u;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (k == 0 || w0 + k < nwo) {
+                    const uint32_t m = nib_mask((k < 4 ? u0 : u1) >> ((k & 3) << 3));
+                    M[s].st(dl, op.dst_row + w0 + k, lane, g0[k] ^ ((g0[k] ^ g1[k]) & m));
+                }
+        }
+    }
+}
+
 // Per-lane argsort arrays (global scratch) for the R1 node.
 struct FastSortSeq {
     uint32_t *glb;
@@ -298,17 +350,22 @@ struct FastSortSeq {
 
 // Prefetch of the per-op operands held in registers.
 struct Pre {
-    uint32_t T;  // f or g table dword of this lane
-    double V;    // leaf: vcl row entry of this lane (lanes < v)
+    uint32_t T;   // f or g table dword of this lane
+    uint32_t T2;  // MF_BFG: the folded parent op's table dword
+    double V;     // leaf: vcl row entry of this lane (lanes < v)
 };
 
 __device__ __forceinline__ Pre fetch_pre(const FastPlan &P, const MOp &op, int lane, int vlane) {
     Pre p;
-    p.T = 0;
+    p.T = p.T2 = 0;
     p.V = 0;
     if (op.type == OP_F || op.type == OP_LEAF_L) p.T = P.f_tab[op.tab * QPD_EXP_TABMUL + (lane & 31)];
-    if (op.type == OP_G || op.type == OP_LEAF_R) p.T = P.g_tab[op.tab * QPD_EXP_TABMUL + lane];
-    if (op.type == OP_BOT3) p.T = P.f_tab[op.tab * QPD_EXP_TABMUL * 32 + (lane & 31)];
+    if ((op.type == OP_G && !(op.flags & MF_GSEL)) || op.type == OP_LEAF_R) p.T = P.g_tab[op.tab * QPD_EXP_TABMUL + lane];
+    if (op.type == OP_BOT3) {
+        p.T = P.f_tab[op.tab * QPD_EXP_TABMUL * 32 + (lane & 31)];
+        if (op.flags & MF_BFG)
+            p.T2 = (op.flags & MF_BG) ? P.g_tab[op.tab2 * QPD_EXP_TABMUL + lane] : P.f_tab[op.tab2 * QPD_EXP_TABMUL + (lane & 31)];
+    }
     if (op.type == OP_LEAF_L || op.type == OP_LEAF_R) p.V = P.vcl[op.vrow + vlane];
     return p;
 }
@@ -461,8 +518,8 @@ __device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], u
 
 template <bool kList, bool L8, int NS>
 __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], const MOp &op,
-                                        const int32_t *const (&y)[NS], Path (&st)[NS], uint32_t Tf0, int gl, int gbase,
-                                        int L, int *sel, int sstride, int lane) {
+                                        const int32_t *const (&y)[NS], Path (&st)[NS], uint32_t Tf0, uint32_t T2, int gl,
+                                        int gbase, int L, int *sel, int sstride, int lane) {
     const int p0 = op.tab * QPD_EXP_TABMUL;
     const int fr = op.cnt;
     const uint32_t *ft = P.f_tab, *gt = P.g_tab;
@@ -483,8 +540,21 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
     const double Vlo = s16 < v ? vb[j16 * v + s16] : 0.0;
     const double Vhi = s16 < v ? vb[(4 + j16) * v + s16] : 0.0;
     uint32_t x[NS][2], c[NS];
+    if (op.flags & MF_BFG) {
+        // The depth n-4 parent's f / g (SCLLUTDecoder.cpp:83-89 / :157-164,
+        // ctemp = 8) folded in: W3 from the parent's 16 symbols, in registers.
+        const bool sl = op.flags & MF_SRC_LDS, ul = op.flags & MF_U_LDS;
 #pragma unroll
-    for (int s = 0; s < NS; ++s) x[s][0] = sym_word(P, M[s], op, y[s], gbase + pfield(st[s].ps, op.sh_src), 0);  // W3
+        for (int s = 0; s < NS; ++s) {
+            const int src = gbase + pfield(st[s].ps, op.sh_src);
+            const uint32_t a = M[s].ld(sl, op.src_row, src), b = M[s].ld(sl, op.src_row + 1, src);
+            const uint32_t ub = (op.flags & MF_BG) ? M[s].ld(ul, op.u_row, gbase + pfield(st[s].pu, op.sh_u)) : 0u;
+            x[s][0] = lut_vec<8>(T2, a, b, ub);
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) x[s][0] = sym_word(P, M[s], op, y[s], gbase + pfield(st[s].ps, op.sh_src), 0);  // W3
+    }
     // ---- q0 left: W2 = f(W3); q1: W1 = f(W2)
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
@@ -518,7 +588,10 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
         const uint32_t c2 = (x[s][1] >> 25) & 3u;
         const uint32_t c3r = (c2 ^ c[s]) | (c[s] << 2);
         const uint32_t c3l = (x[s][1] >> 27) & 15u;
-        M[s].st(op.flags & MF_DST_LDS, op.dst_row, lane, (c3l ^ c3r) | (c3r << 4));  // combine at depth n-3
+        uint32_t res = (c3l ^ c3r) | (c3r << 4);  // combine at depth n-3
+        if (op.flags & MF_BCOMB)  // and the parent's (utils.cpp:62-67): U[n-3] of this lineage ^ res | res
+            res = ((M[s].ld(op.flags & MF_U_LDS, op.u_row, gbase + pfield(st[s].pu, op.sh_u)) & 0xFFu) ^ res) | (res << 8);
+        M[s].st(op.flags & MF_DST_LDS, op.dst_row, lane, res);
         if (!(op.flags & MF_TO_R)) st[s].pu = pset(st[s].pu, op.sh_dst, gl);
     }
 }
@@ -543,40 +616,33 @@ struct LdsSeq16 {
 // Survivor layers of an R1 node (FastSCLLUTDecoder.cpp:118-166) after its
 // argsort: ord[q] / ms[q] = element and magnitude of the q-th smallest |llr|,
 // hw = hard decisions (l < 0).  Each of the m layers forks on flipping the
-// next element; ord/ms/flip follow the surviving lineage, the flip position
-// is the lane's own pre-permutation ord (H2).  Returns the node's bits.
+// next element; ord/ms/flips follow the surviving lineage, the flip position
+// is the slot's own pre-selection ord (H2).  Returns the node's bits.
+// The arrays never move: a slot's lineage holds the arrays its `origin` lane
+// computed (read per layer by two shuffles), and its flips are one bit mask
+// (temp <= 32) shuffled with the survivors -- 5 shuffles a layer, not ~27.
 template <bool L8>
-__device__ __forceinline__ uint32_t r1_layers(Path &st, int *sel, int gl, int gbase, int lane, int L, int m, int (&ord)[kMaxM],
-                                              double (&ms)[kMaxM], uint32_t hw, int temp) {
-    int flip[kMaxM];
-#pragma unroll
-    for (int q = 0; q < kMaxM; ++q) flip[q] = -1;
+__device__ __forceinline__ uint32_t r1_layers(Path &st, int *sel, int gl, int gbase, int lane, int L, int m,
+                                              const int (&ord)[kMaxM], const double (&ms)[kMaxM], uint32_t hw, int temp) {
+    uint32_t flips = 0;
     int origin = gl;
 #pragma unroll
     for (int layer = 0; layer < kMaxM; ++layer) {
         if (layer < m) {
-            const double kf = st.pm + ms[layer];
+            const int o = gbase + origin;
+            const double kf = st.pm + shfld(ms[layer], o);
+            const int pos_old = __shfl(ord[layer], o);  // H2
             const Sel sl = L8 ? select_survivors8(st.pm, kf, gl, gbase, lane, sel)
                               : select_survivors(st.pm, kf, gl, gbase, L, sel);
             const int p = gbase + sl.parent;
-            const int pos_old = ord[layer];  // H2
             st.pm = pick(sl.upper, shfld(kf, p), shfld(st.pm, p));
             st.ps = shfl64(st.ps, p);
             st.pu = shfl64(st.pu, p);
             origin = __shfl(origin, p);
-#pragma unroll
-            for (int q = 0; q < kMaxM; ++q) {
-                ord[q] = __shfl(ord[q], p);
-                ms[q] = shfld(ms[q], p);
-                if (q < layer) flip[q] = __shfl(flip[q], p);
-            }
-            flip[layer] = sl.upper ? pos_old : -1;
+            flips = (uint32_t)__shfl((int)flips, p) ^ (sl.upper ? 1u << (pos_old & 31) : 0u);
         }
     }
-    uint32_t word = (uint32_t)__shfl((int)hw, gbase + origin);
-#pragma unroll
-    for (int q = 0; q < kMaxM; ++q)
-        if (q < m && flip[q] >= 0) word ^= 1u << (flip[q] & 31);
+    const uint32_t word = (uint32_t)__shfl((int)hw, gbase + origin) ^ flips;
     return temp < 32 ? word & ((1u << temp) - 1u) : word;
 }
 
@@ -921,7 +987,7 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QP
             for (int s = 0; s < NS; ++s) {
                 int64_t f = (task * NS + s) * fpw + (lane >> gsh);
                 if (f >= B) f = B - 1;
-                yv[s] = in + (f << P.n);
+                yv[s] = in + (f << P.in_shift);
             }
             if (nxt.flags & MF_SYNC) wave_sync();  // before the next prefetch is issued
             const MOp op = nxt;
@@ -937,7 +1003,7 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QP
             const int fl = op.flags;
             switch (op.type) {
                 case OP_BOT3:
-                    bot3_op<kList, L8>(P, Mv, op, yv, stv, cur.T, gl, gbase, L, sel_all, sstride, lane);
+                    bot3_op<kList, L8>(P, Mv, op, yv, stv, cur.T, cur.T2, gl, gbase, L, sel_all, sstride, lane);
                     break;
                 case OP_F:
                 case OP_G: {
@@ -947,7 +1013,9 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QP
                         src[s] = gbase + pfield(stv[s].ps, op.sh_src);
                         usrc[s] = gbase + pfield(stv[s].pu, op.sh_u);
                     }
-                    if (op.type == OP_F)
+                    if (fl & MF_GSEL)
+                        gsel_op(Mv, op, yv, usrc, lane);
+                    else if (op.type == OP_F)
                         fg_op<false>(P, Mv, op, yv, src, usrc, cur.T, lane);
                     else
                         fg_op<true>(P, Mv, op, yv, src, usrc, cur.T, lane);
@@ -1151,6 +1219,47 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QP
             atomicAdd(&qpd_stamp_acc[32 + threadIdx.x], (unsigned long long)stamp_cnt);
         }
 #endif
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Root pre-pass (pre-mode: N >= 16, the root's left child a plain node).
+// The root's f and both g variants depend on the channel symbols only, yet
+// every path of a frame computes them (SCLLUTDecoder.cpp:83-89 / :157-164 at
+// depth 0: L x N lookups per frame), and the decode kernel would read the
+// frame's 4 KB of int32 symbols twice, half a decode apart.  Here one thread
+// per output word computes them once per frame from one coalesced read of the
+// channel, into a row of N/4 words per frame: [f(y) | g(y, 0) | g(y, 1) | -],
+// N/16 words each, 8 nibble symbols per word as S[1].  The decode kernel then
+// reads the left child's S[1] from the row (MF_PRE) and builds the root g by
+// nibble selects (MF_GSEL, gsel_op).  Out-of-range symbols raise the error
+// flag here, as chan_word8 does in the decode kernel.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void root_pre_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
+                                                       uint32_t *__restrict__ pre) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t Tf = P.f_tab[lane & 31], Tg = P.g_tab[lane];  // node 0 (posi 0)
+    const int wsh = P.n - 4;                                      // log2 words per segment
+    const int half = P.N >> 1;
+    const int64_t total = B << wsh;
+    for (int64_t base = (int64_t)blockIdx.x * 256; base < total; base += (int64_t)gridDim.x * 256) {
+        // whole waves stay active through the ds_bpermute lookups (inactive lanes read as 0)
+        const int64_t t0 = base + threadIdx.x;
+        const int64_t t = t0 < total ? t0 : total - 1;
+        const int64_t f = t >> wsh;
+        const int w = (int)(t & ((1 << wsh) - 1));
+        const int32_t *y = in + (f << P.n);
+        const uint32_t a = chan_word8(y, 8 * w, P.in_vec, P.v, P.err);
+        const uint32_t b = chan_word8(y, half + 8 * w, P.in_vec, P.v, P.err);
+        const uint32_t fw = lut_vec<8>(Tf, a, b, 0u);
+        const uint32_t g0 = lut_vec<8>(Tg, a, b, 0u);
+        const uint32_t g1 = lut_vec<8>(Tg, a, b, 0xFFu);
+        if (t0 < total) {
+            uint32_t *row = pre + (f << (P.n - 2));
+            row[w] = fw;
+            row[(1 << wsh) + w] = g0;
+            row[(2 << wsh) + w] = g1;
+        }
     }
 }
 

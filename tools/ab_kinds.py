@@ -26,5 +26,6 @@ for kind in kinds:
         e1.record()
         torch.cuda.synchronize()
         best = min(best, e0.elapsed_time(e1))
-    print(f"{os.path.basename(os.environ.get('QPD_LIB', 'libqpd.so')):24s} {kind:12s} {best:8.3f} ms "
+    tag = os.environ.get("AB_TAG") or os.path.basename(os.environ.get("QPD_LIB", "libqpd.so"))
+    print(f"{tag:30s} {kind:12s} {best:8.3f} ms "
           f"{F / best / 1e3:8.3f} Mframes/s digest {dig}", flush=True)
