@@ -258,6 +258,9 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": hbm_bytes,
+                         "kernels": "one decode call = root_pre_kernel + lut_fast_kernel on the bench stream "
+                                    "(HIP events bracket both; traffic sums both)" if info["engine"] == 2 else
+                                    "generic_decode_kernel",
                          "onchip_lds_equiv": {"achieved": onchip, "peak": LDS_PEAK_GBS, "unit": "GB/s",
                                               "frac": onchip / LDS_PEAK_GBS,
                                               "bytes_per_frame": LOOKUPS_PER_FRAME * ONCHIP_BYTES_PER_LOOKUP}},

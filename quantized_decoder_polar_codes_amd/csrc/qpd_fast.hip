@@ -1095,7 +1095,14 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QP
             __builtin_amdgcn_s_waitcnt(0);
             {
                 const uint64_t dt = __builtin_amdgcn_s_memtime() - stamp_t0;
+#ifdef QPD_STAMPS_DEPTH  // F / G / COMB by depth: 0-7 / 8-15 / 16-23; BOT3 24; leaves 25; specials 26-29
+                const int dd = op.d < 7 ? op.d : 7;
+                const int cls = op.type == OP_F ? dd : op.type == OP_G ? 8 + dd : op.type == OP_COMB ? 16 + dd
+                              : op.type == OP_BOT3 ? 24 : (op.type == OP_LEAF_L || op.type == OP_LEAF_R) ? 25
+                              : 26 + (op.type - OP_R0) % 4;
+#else
                 const int cls = op.type == OP_R1 ? 24 + (op.cnt > 16) + (op.cnt > 8) : 2 * op.type + ((fl & MF_SYNC) ? 1 : 0);
+#endif
                 if ((int)(threadIdx.x & 31) == cls) stamp_acc += dt;
                 if ((int)(threadIdx.x & 31) == cls) stamp_cnt += 1;
             }
