@@ -496,41 +496,90 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     F.max_r1 = s.max_r1;
     auto srows = [&](int dd) { return std::max(1, (N >> dd) / 8); };
     auto brows = [&](int dd) { return std::max(1, (N >> dd) / 32); };
+    // Row slots per depth: 0 = R, 1 = S, 2 = U.  `use` keeps all of them, or
+    // (trimmed layout) only those some op touches: BOT3 subtrees keep depths
+    // n-2..n in registers and the fused BOT3s also skip S/R[n-3], which frees
+    // LDS for a shallower lds_from.
+    bool use[3][qpd::kMaxDepth + 1];
+    for (auto &u : use)
+        for (bool &b : u) b = true;
+    auto rows_of = [&](int slot, int dd) {
+        if (slot == 1) return (dd >= 1 && dd <= n - 1) ? srows(dd) : 0;
+        if (slot == 2) return dd >= 1 ? brows(dd) : 0;
+        return brows(dd);
+    };
     auto lds_rows = [&](int D) {
         int r = 0;
-        for (int dd = std::max(D, 1); dd <= n - 1; ++dd) r += srows(dd);
-        for (int dd = std::max(D, 1); dd <= n; ++dd) r += brows(dd);
-        for (int dd = D; dd <= n; ++dd) r += brows(dd);
+        for (int dd = D; dd <= n; ++dd)
+            for (int sl = 0; sl < 3; ++sl)
+                if (use[sl][dd]) r += rows_of(sl, dd);
         return r;
+    };
+    auto assign = [&](FastLayout &L, int &rl, int &rg) {
+        rl = rg = 0;
+        for (int dd = 0; dd <= n; ++dd) {  // grouped by depth (see FastLayout)
+            int &r = L.lds(dd) ? rl : rg;
+            if (L.lds(dd)) L.lds_base[dd] = r;
+            L.R[dd] = r;
+            if (use[0][dd]) r += rows_of(0, dd);
+            L.S[dd] = r;
+            if (use[1][dd]) r += rows_of(1, dd);
+            L.U[dd] = r;
+            if (use[2][dd]) r += rows_of(2, dd);
+        }
+        L.lds_base[n + 1] = rl;
+        L.lds_end = rl + qpd::kSelInts / 64;
     };
     d->sets = c->kind == QPD_FASTSCL_LUT ? 1 : kDefaultSets;  // FastSCL's R1 argsort state spills at NS = 2
     if (const char *e = getenv("QPD_SETS")) d->sets = std::min(2, std::max(1, atoi(e)));
     d->l8 = (c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT) && d->L == 8;
     const int NS = d->sets;
+    FastLayout Ly;
+    const int32_t *nt_fast = (c->kind == QPD_FASTSC_LUT || c->kind == QPD_FASTSCL_LUT) ? c->node_type : nullptr;
+    // pre-mode: S[1] is whole words (N >= 16) and the root's left child a plain node
+    Ly.pre = n >= 4 && special_of(c->kind, nt_fast, 1) < 0 && !getenv("QPD_NO_PRE");
+    Ly.bfuse = !getenv("QPD_NO_BFUSE");
+    // Trimmed layout, except where FastSCL's R1 argsorts (> 16 elements) use
+    // the LDS rows of the deeper levels as scratch: probe the op list on an
+    // all-global layout and keep the slots it touches.
+    if (!(c->kind == QPD_FASTSCL_LUT && s.max_r1 > qpd::stl::kThreshold) && !getenv("QPD_NO_TRIM")) {
+        FastLayout Lp = Ly;
+        Lp.D = n + 1;
+        int pl = 0, pg = 0;
+        assign(Lp, pl, pg);
+        std::vector<qpd::MOp> probe;
+        std::vector<uint16_t> r1p;
+        fast_ops(probe, Lp, c->kind, N, n, v, c->frozen_bits, nt_fast, c->vcl, r1p, 0, 0);
+        std::vector<int> owner(std::max(pg, 1), -1);  // row -> slot * 32 + depth
+        for (int dd = 0; dd <= n; ++dd)
+            for (int sl = 0; sl < 3; ++sl) {
+                const int b = sl == 0 ? Lp.R[dd] : sl == 1 ? Lp.S[dd] : Lp.U[dd];
+                for (int r = 0; r < rows_of(sl, dd); ++r) owner[b + r] = sl * 32 + dd;
+            }
+        bool used[3][qpd::kMaxDepth + 1] = {};
+        auto mark = [&](int row) {
+            if (row >= 0 && row < pg && owner[row] >= 0) used[owner[row] / 32][owner[row] % 32] = true;
+        };
+        for (const qpd::MOp &m : probe) {
+            using namespace qpd;
+            if (!(m.flags & (MF_CHAN | MF_PRE))) mark(m.src_row);
+            mark(m.dst_row);
+            if (m.type == OP_G || m.type == OP_LEAF_R || m.type == OP_COMB ||
+                (m.type == OP_BOT3 && (m.flags & (MF_BG | MF_BCOMB))))
+                mark(m.u_row);
+            if (m.type == OP_COMB) mark(m.r_row);
+        }
+        used[0][0] = true;  // R[0]: the tail re-encodes it
+        std::memcpy(use, used, sizeof(use));
+    }
     // LDS per wave = NS * (selection scratch + rows of depths >= D); the budget
     // is measured: occupancy beats LDS residency of the shallow depths.
     int budget = NS == 1 ? 6 * 1024 : 10 * 1024;
     if (const char *e = getenv("QPD_LDS_BUDGET")) budget = atoi(e);
-    FastLayout Ly;
     while (Ly.D <= n && NS * (qpd::kSelInts * 4 + lds_rows(Ly.D) * 256) > budget) ++Ly.D;
     F.lds_from = Ly.D;
     int rl = 0, rg = 0;
-    for (int dd = 0; dd <= n; ++dd) {  // grouped by depth (see FastLayout)
-        int &r = Ly.lds(dd) ? rl : rg;
-        if (Ly.lds(dd)) Ly.lds_base[dd] = r;
-        Ly.R[dd] = r;
-        r += brows(dd);
-        if (dd >= 1 && dd <= n - 1) {
-            Ly.S[dd] = r;
-            r += srows(dd);
-        }
-        if (dd >= 1) {
-            Ly.U[dd] = r;
-            r += brows(dd);
-        }
-    }
-    Ly.lds_base[n + 1] = rl;
-    Ly.lds_end = rl + qpd::kSelInts / 64;
+    assign(Ly, rl, rg);
     F.R0_row = Ly.R[0];
     F.R0_lds = Ly.lds(0);
     F.H_row = F.K_row = F.I_row = rg;
@@ -547,10 +596,6 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     d->lds_bytes = NS * (qpd::kSelInts * 4 + rl * 256);
     std::vector<qpd::MOp> mops;
     std::vector<uint16_t> r1tab;
-    const int32_t *nt_fast = (c->kind == QPD_FASTSC_LUT || c->kind == QPD_FASTSCL_LUT) ? c->node_type : nullptr;
-    // pre-mode: S[1] is whole words (N >= 16) and the root's left child a plain node
-    Ly.pre = n >= 4 && special_of(c->kind, nt_fast, 1) < 0 && !getenv("QPD_NO_PRE");
-    Ly.bfuse = !getenv("QPD_NO_BFUSE");
     d->pre = Ly.pre;
     d->pre_chunk = std::max<int64_t>(1, ((int64_t)256 << 20) / N);  // pre-pass rows: N bytes per frame, <= 256 MB
     if (const char *e = getenv("QPD_PRE_CHUNK")) d->pre_chunk = std::max<int64_t>(1, atoll(e));
