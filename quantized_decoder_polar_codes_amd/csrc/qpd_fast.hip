@@ -981,13 +981,18 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QP
             const int gl = lane & (gs - 1);
             const int gbase = lane & ~(gs - 1);
             const int vlane = lane < P.v ? lane : 0;
-            const int32_t *yv[NS];  // channel rows (read by MF_CHAN ops only)
+            const int32_t *yv[NS];  // frame rows of `in` (read by MF_CHAN / MF_PRE ops only)
             const int gsh = __builtin_ctz(gs);
+            if (nxt.flags & (MF_CHAN | MF_PRE)) {  // wave-uniform: no per-lane address math on other ops
 #pragma unroll
-            for (int s = 0; s < NS; ++s) {
-                int64_t f = (task * NS + s) * fpw + (lane >> gsh);
-                if (f >= B) f = B - 1;
-                yv[s] = in + (f << P.in_shift);
+                for (int s = 0; s < NS; ++s) {
+                    int64_t f = (task * NS + s) * fpw + (lane >> gsh);
+                    if (f >= B) f = B - 1;
+                    yv[s] = in + (f << P.in_shift);
+                }
+            } else {
+#pragma unroll
+                for (int s = 0; s < NS; ++s) yv[s] = in;
             }
             if (nxt.flags & MF_SYNC) wave_sync();  // before the next prefetch is issued
             const MOp op = nxt;
