@@ -120,6 +120,14 @@ struct Mem {
     }
 };
 
+// Table dword `at + ldw` (at wave-uniform, ldw = the lane's dword) through a
+// buffer descriptor: the uniform part rides in the SGPR offset, so a table
+// fetch costs no per-lane 64-bit address arithmetic.
+__device__ __forceinline__ uint32_t tab_ld(const uint32_t *base, int at, int ldw) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)base, 0, 0x7fffffff, 0x00020000);
+    return __builtin_amdgcn_raw_buffer_load_b32(r, ldw * 4, at * 4, 0);
+}
+
 __device__ __forceinline__ uint32_t bperm(uint32_t table, uint32_t dword) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(dword << 2), (int)table);
 }
@@ -359,12 +367,13 @@ __device__ __forceinline__ Pre fetch_pre(const FastPlan &P, const MOp &op, int l
     Pre p;
     p.T = p.T2 = 0;
     p.V = 0;
-    if (op.type == OP_F || op.type == OP_LEAF_L) p.T = P.f_tab[op.tab * QPD_EXP_TABMUL + (lane & 31)];
-    if ((op.type == OP_G && !(op.flags & MF_GSEL)) || op.type == OP_LEAF_R) p.T = P.g_tab[op.tab * QPD_EXP_TABMUL + lane];
+    if (op.type == OP_F || op.type == OP_LEAF_L) p.T = tab_ld(P.f_tab, op.tab * QPD_EXP_TABMUL, lane & 31);
+    if ((op.type == OP_G && !(op.flags & MF_GSEL)) || op.type == OP_LEAF_R) p.T = tab_ld(P.g_tab, op.tab * QPD_EXP_TABMUL, lane);
     if (op.type == OP_BOT3) {
-        p.T = P.f_tab[op.tab * QPD_EXP_TABMUL * 32 + (lane & 31)];
+        p.T = tab_ld(P.f_tab, op.tab * QPD_EXP_TABMUL * 32, lane & 31);
         if (op.flags & MF_BFG)
-            p.T2 = (op.flags & MF_BG) ? P.g_tab[op.tab2 * QPD_EXP_TABMUL + lane] : P.f_tab[op.tab2 * QPD_EXP_TABMUL + (lane & 31)];
+            p.T2 = (op.flags & MF_BG) ? tab_ld(P.g_tab, op.tab2 * QPD_EXP_TABMUL, lane)
+                                      : tab_ld(P.f_tab, op.tab2 * QPD_EXP_TABMUL, lane & 31);
     }
     if (op.type == OP_LEAF_L || op.type == OP_LEAF_R) p.V = P.vcl[op.vrow + vlane];
     return p;
@@ -526,12 +535,12 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
     // Tables of the 7 internal nodes (q0's f table arrives prefetched).  Two
     // 32-dword f tables share one register (lanes 0-31 | 32-63: p and p+1 are
     // adjacent), addressed by adding 256 to the nibble index of the second.
-    const uint32_t Tg0 = gt[(size_t)p0 * 64 + lane];
+    const uint32_t Tg0 = tab_ld(gt, p0 * 64, lane);
     const int p1 = 2 * p0 + 1, p3 = 4 * p0 + 3;
-    const uint32_t Tf12 = ft[(size_t)p1 * 32 + lane], Tg1 = gt[(size_t)p1 * 64 + lane], Tg2 = gt[(size_t)(p1 + 1) * 64 + lane];
-    const uint32_t Tf34 = ft[(size_t)p3 * 32 + lane], Tg3 = gt[(size_t)p3 * 64 + lane], Tg4 = gt[(size_t)(p3 + 1) * 64 + lane];
-    const uint32_t Tf56 = ft[(size_t)(p3 + 2) * 32 + lane], Tg5 = gt[(size_t)(p3 + 2) * 64 + lane],
-                   Tg6 = gt[(size_t)(p3 + 3) * 64 + lane];
+    const uint32_t Tf12 = tab_ld(ft, p1 * 32, lane), Tg1 = tab_ld(gt, p1 * 64, lane), Tg2 = tab_ld(gt, (p1 + 1) * 64, lane);
+    const uint32_t Tf34 = tab_ld(ft, p3 * 32, lane), Tg3 = tab_ld(gt, p3 * 64, lane), Tg4 = tab_ld(gt, (p3 + 1) * 64, lane);
+    const uint32_t Tf56 = tab_ld(ft, (p3 + 2) * 32, lane), Tg5 = tab_ld(gt, (p3 + 2) * 64, lane),
+                   Tg6 = tab_ld(gt, (p3 + 3) * 64, lane);
     // Leaf quanta vcl[n-1][8*node + j][s] of the 8 leaves, four leaves per
     // register: lane 16*jj + s holds leaf 4*h + jj (v <= 16).
     const int v = P.v;
