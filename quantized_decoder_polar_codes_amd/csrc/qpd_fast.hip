@@ -108,11 +108,23 @@ struct Mem {
     uint32_t *lds;
     uint32_t *gp;               // slab base (R1 argsort arrays)
     __amdgpu_buffer_rsrc_t rs;  // the same slab as a buffer resource
+    // `row` wave-uniform: it rides in the buffer op's SGPR offset
     __device__ __forceinline__ uint32_t ld(bool in_lds, int row, int lane) const {
+        if (in_lds) return lds[row * 64 + lane];
+        return __builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, row * 256, QPD_SLAB_AUX);
+    }
+    __device__ __forceinline__ void st(bool in_lds, int row, int lane, uint32_t v) const {
+        if (in_lds)
+            lds[row * 64 + lane] = v;
+        else
+            __builtin_amdgcn_raw_buffer_store_b32(v, rs, lane * 4, row * 256, QPD_SLAB_AUX);
+    }
+    // any row (per-lane)
+    __device__ __forceinline__ uint32_t ldv(bool in_lds, int row, int lane) const {
         if (in_lds) return lds[row * 64 + lane];
         return __builtin_amdgcn_raw_buffer_load_b32(rs, (row * 64 + lane) * 4, 0, QPD_SLAB_AUX);
     }
-    __device__ __forceinline__ void st(bool in_lds, int row, int lane, uint32_t v) const {
+    __device__ __forceinline__ void stv(bool in_lds, int row, int lane, uint32_t v) const {
         if (in_lds)
             lds[row * 64 + lane] = v;
         else
@@ -892,7 +904,7 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
         }
         if (parity) {
             const int row = op.dst_row + (bi >> 5);
-            M.st(dl, row, lane, M.ld(dl, row, lane) ^ (1u << (bi & 31)));
+            M.stv(dl, row, lane, M.ldv(dl, row, lane) ^ (1u << (bi & 31)));  // bi: per lane
         }
     } else if (!kList) {  // OP_R1, FastSC: `<= 0`
         uint32_t word = 0;
@@ -1180,7 +1192,7 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QP
             if (split) {
                 uint32_t x[8];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) x[k] = k < wpl ? polar_word(M.ld(rl, r0 + gl * wpl + k, src)) : 0u;
+                for (int k = 0; k < 8; ++k) x[k] = k < wpl ? polar_word(M.ldv(rl, r0 + gl * wpl + k, src)) : 0u;
 #pragma unroll
                 for (int mw = 1; mw < 8; mw *= 2)  // word stages inside the lane
 #pragma unroll
@@ -1202,7 +1214,7 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QP
             if (frame < B) {
                 auto bit = [&](int pos) {
                     const int w = pos >> 5;
-                    const uint32_t x = split ? M.lds[(w & (wpl - 1)) * 64 + gbase + (w >> wsh)] : M.ld(rl, r0 + w, src);
+                    const uint32_t x = split ? M.lds[(w & (wpl - 1)) * 64 + gbase + (w >> wsh)] : M.ldv(rl, r0 + w, src);
                     return (x >> (pos & 31)) & 1u;
                 };
                 if (dword_out) {
