@@ -245,7 +245,8 @@ __device__ __forceinline__ uint32_t lut_vec(uint32_t T, uint32_t A, uint32_t B, 
     for (int k = 0; k < NE; ++k) {
         const int j = k >> 1;
         const uint32_t WA = (k & 1) ? YA : XA, WS = (k & 1) ? YS : XS;
-        const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((WA >> (8 * j)) & 0xFFu), (int)T);
+        // ds_bpermute reads lane (addr >> 2) & 63: the bytes above j need no mask
+        const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(WA >> (8 * j)), (int)T);
         out |= __builtin_amdgcn_ubfe(v, WS >> (8 * j), 4) << (4 * k);
     }
     return out;
