@@ -722,7 +722,7 @@ __device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const 
                 seq.set(j, (int)(((e >> 1) << 5) | (uint32_t)j));
             }
         }
-        stl::sort_small(seq, 0, temp);
+        stl::sort_small_prefix(seq, 0, temp, m);  // only ord[0, m) is read
 #pragma unroll
         for (int q = 0; q < kMaxM; ++q)
             if (q < m) ord[q] = seq.get(q) & 31;

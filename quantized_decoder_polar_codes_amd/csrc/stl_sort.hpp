@@ -222,6 +222,39 @@ QPD_HD void sort_small(Seq &s, int first, int last) {
     final_insertion_sort(s, first, last);
 }
 
+// sort_small when only the first m outputs are read (the R1 node's m = min(L-1,
+// temp) survivor layers): the same steps, minus those that cannot reach them.
+// A partition leaves [first, cut) <= pivot <= [cut, last), and no later step
+// moves an element of a right block before an element of a left block (the
+// guarded insertion's `val < *first` and the unguarded insertion's
+// `val < *prev` are false across such a boundary).  So once a block boundary c
+// with c - first >= m is known, the order of [first, c) is final-insertion-sort
+// of [first, c) alone: the right part's partitioning and its insertions are
+// skipped.  Positions >= c of the array are left unsorted.
+template <class Seq>
+QPD_HD void sort_small_prefix(Seq &s, int first, int last, int m) {
+    if (first == last) return;
+    int f = first, l = last, dl = lg(last - first) * 2, end = last;
+    while (l - f > kThreshold) {
+        if (dl == 0) {
+            heap_sort(s, f, l);
+            break;
+        }
+        --dl;
+        const int mid = f + (l - f) / 2;
+        move_median_to_first(s, f, f + 1, mid, l - 1);
+        const int cut = unguarded_partition(s, f + 1, l, f);
+        if (cut - first >= m && cut < end) end = cut;  // a block boundary past the needed prefix
+        if (l - cut > kThreshold) {
+            if (cut >= end) break;  // the reference's recursion on [cut, l) lies past the prefix
+            f = cut;
+        } else {
+            l = cut;
+        }
+    }
+    final_insertion_sort(s, first, end);
+}
+
 template <class Seq>
 QPD_HD void sort(Seq &s, int first, int last) {
     if (first == last) return;

@@ -44,6 +44,15 @@ int main(int argc, char **argv) {
             VecSeq s2{c, key};
             qpd::stl::sort_small(s2, 0, n);
             if (a != c && ++bad < 5) printf("sort_small mismatch n=%d distinct=%d\n", n, distinct);
+            for (int m = 1; m <= 8; ++m) {  // the R1 layers read the first min(L-1, n) entries
+                std::vector<int> e(n);
+                for (int i = 0; i < n; ++i) e[i] = i;
+                VecSeq s3{e, key};
+                qpd::stl::sort_small_prefix(s3, 0, n, m);
+                const int k = std::min(m, n);
+                if (!std::equal(a.begin(), a.begin() + k, e.begin()) && ++bad < 5)
+                    printf("sort_small_prefix mismatch n=%d m=%d distinct=%d\n", n, m, distinct);
+            }
         }
     }
     printf("trials=%ld mismatches=%ld\n", trials, bad);
