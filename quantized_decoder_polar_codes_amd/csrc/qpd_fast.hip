@@ -411,6 +411,13 @@ __device__ unsigned long long qpd_sel_stats[64];
 #endif
 constexpr int kSelInts = 128;  // per set: 64 slots + 64 junk slots (select_survivors8)
 
+// max of two non-negative doubles given as bits (one v_max_f64).
+__device__ __forceinline__ uint64_t dmax_bits(uint64_t a, uint64_t b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(__builtin_bit_cast(double, a)), "v"(__builtin_bit_cast(double, b)));
+    return __builtin_bit_cast(uint64_t, r);
+}
+
 // Info leaf with quanta dm: keep the L best of {keep, flip} candidates.
 // Returns the new decision; `extra` words follow the surviving lineage.
 template <bool L8, int NX>
@@ -449,14 +456,15 @@ __device__ __forceinline__ uint32_t leaf_fork(Path &st, double dm, int gl, int g
         // in stable order (pm_0 <= ... <= pm_7) and no flip beats any keep
         // (max pm <= every kf).  The stable sort of the 16 candidates then
         // puts keep_j in slot j: nothing moves, the decision is the hard one.
+        // Path metrics are >= +0 or +inf, never NaN (a NaN metric raises ERR_NAN_PM in
+        // the generic engine; LUT quanta are finite): max over doubles = max over
+        // their bits.  v_max_f64 by inline asm: the builtin would canonicalize the
+        // DPP results first (two more VALU per step).
         const uint64_t K = __builtin_bit_cast(uint64_t, st.pm), F = __builtin_bit_cast(uint64_t, kf);
         uint64_t mk = K;
-        uint64_t o = dpp64<kDppXor1>(mk);
-        mk = o > mk ? o : mk;
-        o = dpp64<kDppXor2>(mk);
-        mk = o > mk ? o : mk;
-        o = dpp64<kDppHalfMirror>(mk);  // lane i^7 lies in the other quad
-        mk = o > mk ? o : mk;
+        mk = dmax_bits(mk, dpp64<kDppXor1>(mk));
+        mk = dmax_bits(mk, dpp64<kDppXor2>(mk));
+        mk = dmax_bits(mk, dpp64<kDppHalfMirror>(mk));  // lane i^7 lies in the other quad
         const uint64_t Kn = dpp64<kDppRowShl1>(K);  // pm of slot gl+1
         const bool ok = F >= mk && (gl == 7 || K <= Kn);
         if (__ballot(ok) == ~0ull) return hd;
