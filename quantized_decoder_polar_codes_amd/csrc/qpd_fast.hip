@@ -494,7 +494,9 @@ __device__ __forceinline__ void leaf_decide(Path (&st)[NS], const double (&dm)[N
     if (frozen) {
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            st[s].pm += fabs(dm[s]) * (double)(dm[s] < 0);  // :100-104
+            // :100-104, |dm|·(dm<0) as a select: the same double (|dm|·1 = |dm|,
+            // |dm|·0 = +0, and pm is never -0)
+            st[s].pm += dm[s] < 0 ? fabs(dm[s]) : 0.0;
             dec[s] = 0u;
         }
         return;
@@ -845,7 +847,7 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
                 llr8(w, l, word);
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
-                    if (8 * w + i < temp) st.pm += (double)(float)(l[i] < 0) * fabs(l[i]);  // H5
+                    if (8 * w + i < temp) st.pm += l[i] < 0 ? fabs(l[i]) : 0.0;  // H5; (float)(l<0)·|l| as a select
             }
         }
         for (int w = 0; w < nwo; ++w) M.st(dl, op.dst_row + w, lane, 0u);
@@ -871,8 +873,8 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
                     if (8 * w + i < temp) {
-                        kk += (double)(l[i] < 0) * fabs(l[i]);
-                        kf += (double)(l[i] >= 0) * fabs(l[i]);
+                        kk += l[i] < 0 ? fabs(l[i]) : 0.0;  // (l<0)·|l|, (l>=0)·|l| as selects
+                        kf += l[i] >= 0 ? fabs(l[i]) : 0.0;
                     }
             }
             const Sel sx = L8 ? select_survivors8(kk, kf, gl, gbase, lane, sel) : select_survivors(kk, kf, gl, gbase, L, sel);
