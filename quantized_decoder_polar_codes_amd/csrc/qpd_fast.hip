@@ -264,22 +264,40 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
     const bool dl = op.flags & MF_DST_LDS, ul = op.flags & MF_U_LDS;
     if (ctemp >= 64) {
         const int nwo = ctemp >> 3;  // multiple of 8
+        if constexpr (NS == 2) {
+            // chunks of 4 words of both sets: the sets' loads are in flight together
+            for (int w0 = 0; w0 < nwo; w0 += 4) {
+                uint32_t A[NS][4], B[NS][4], ub[NS];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
+                for (int s = 0; s < NS; ++s) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        A[s][k] = sym_word(P, M[s], op, y[s], src[s], w0 + k);
+                        B[s][k] = sym_word(P, M[s], op, y[s], src[s], nwo + w0 + k);
+                    }
+                    ub[s] = ISG ? M[s].ld(ul, op.u_row + (w0 >> 2), usrc[s]) : 0u;
+                }
+#pragma unroll
+                for (int s = 0; s < NS; ++s)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        M[s].st(dl, op.dst_row + w0 + k, lane, lut_vec<8>(T, A[s][k], B[s][k], ub[s] >> (k << 3)));
+            }
+        } else {
             for (int w0 = 0; w0 < nwo; w0 += 8) {
                 uint32_t A[8], B[8], ub[2] = {0u, 0u};
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
-                    A[k] = sym_word(P, M[s], op, y[s], src[s], w0 + k);
-                    B[k] = sym_word(P, M[s], op, y[s], src[s], nwo + w0 + k);
+                    A[k] = sym_word(P, M[0], op, y[0], src[0], w0 + k);
+                    B[k] = sym_word(P, M[0], op, y[0], src[0], nwo + w0 + k);
                 }
                 if (ISG) {
-                    ub[0] = M[s].ld(ul, op.u_row + (w0 >> 2), usrc[s]);
-                    ub[1] = M[s].ld(ul, op.u_row + (w0 >> 2) + 1, usrc[s]);
+                    ub[0] = M[0].ld(ul, op.u_row + (w0 >> 2), usrc[0]);
+                    ub[1] = M[0].ld(ul, op.u_row + (w0 >> 2) + 1, usrc[0]);
                 }
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
-                    M[s].st(dl, op.dst_row + w0 + k, lane, lut_vec<8>(T, A[k], B[k], ub[k >> 2] >> ((k & 3) << 3)));
+                    M[0].st(dl, op.dst_row + w0 + k, lane, lut_vec<8>(T, A[k], B[k], ub[k >> 2] >> ((k & 3) << 3)));
             }
         }
     } else if (ctemp >= 8) {
