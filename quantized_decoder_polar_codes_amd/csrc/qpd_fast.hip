@@ -1118,16 +1118,31 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QP
 #pragma unroll
                         for (int s = 0; s < NS; ++s) Mv[s].st(dl, op.dst_row, lane, (u[s] ^ r[s]) | (r[s] << ctemp));
                     } else {
-                        const int cw = ctemp >> 5;
+                        const int cw = ctemp >> 5;  // 1, 2 or a multiple of 4
+                        int usrc[NS];
 #pragma unroll
-                        for (int s = 0; s < NS; ++s) {
-                            const int usrc = gbase + pfield(stv[s].pu, op.sh_u);
-                            for (int w = 0; w < cw; ++w) {
-                                const uint32_t u = Mv[s].ld(ul, op.u_row + w, usrc);
-                                const uint32_t r = Mv[s].ld(rl, op.r_row + w, lane);
-                                Mv[s].st(dl, op.dst_row + w, lane, u ^ r);
-                                Mv[s].st(dl, op.dst_row + cw + w, lane, r);
-                            }
+                        for (int s = 0; s < NS; ++s) usrc[s] = gbase + pfield(stv[s].pu, op.sh_u);
+                        // 4 words of every set per round: all their loads in flight together
+                        for (int w0 = 0; w0 < cw; w0 += 4) {
+                            uint32_t u[NS][4], r[NS][4];
+#pragma unroll
+                            for (int s = 0; s < NS; ++s)
+#pragma unroll
+                                for (int k = 0; k < 4; ++k) {
+                                    u[s][k] = r[s][k] = 0u;
+                                    if (k == 0 || w0 + k < cw) {
+                                        u[s][k] = Mv[s].ld(ul, op.u_row + w0 + k, usrc[s]);
+                                        r[s][k] = Mv[s].ld(rl, op.r_row + w0 + k, lane);
+                                    }
+                                }
+#pragma unroll
+                            for (int s = 0; s < NS; ++s)
+#pragma unroll
+                                for (int k = 0; k < 4; ++k)
+                                    if (k == 0 || w0 + k < cw) {
+                                        Mv[s].st(dl, op.dst_row + w0 + k, lane, u[s][k] ^ r[s][k]);
+                                        Mv[s].st(dl, op.dst_row + cw + w0 + k, lane, r[s][k]);
+                                    }
                         }
                     }
                     if (!(fl & MF_TO_R)) {
