@@ -7,7 +7,8 @@
   symbols are still reported (the pre-pass reads the channel now);
 * fused BOT3 ops (the depth n-4 node's f / g and combine folded into its
   BOT3 children) -- on and off (QPD_NO_BFUSE), with their rows in LDS or in
-  the global slab."""
+  the global slab;
+* N up to 4096 (R1 nodes above 32 elements: the untrimmed layout)."""
 import numpy as np
 import pytest
 
@@ -31,7 +32,15 @@ def qpd(native_lib):
 def _node_type(N, K):
     from quantized_decoder_polar_codes_amd import codes as C
 
-    _, mb, fm, mm = C.construct_pw(N, K)
+    if N <= 1024:
+        _, mb, fm, mm = C.construct_pw(N, K)
+    else:  # beyond the 5G sequence: BEC(1/2) Bhattacharyya construction, the N-K worst frozen
+        z = np.array([0.5])
+        while z.size < N:
+            z = np.stack([2 * z - z * z, z * z], axis=1).reshape(-1)
+        fm = np.zeros(N, dtype=np.int64)
+        fm[np.argsort(-z, kind="stable")[: N - K]] = 1
+        mb = np.flatnonzero(fm == 0)
     return fm, C.identify_nodes(N, mb).astype(np.int32)
 
 
@@ -42,7 +51,8 @@ def _set_env(monkeypatch, env):
         monkeypatch.setenv(k, v)
 
 
-@pytest.mark.parametrize("N,K,L", [(16, 8, 4), (32, 12, 8), (64, 40, 3), (128, 64, 8), (1024, 512, 8)])
+@pytest.mark.parametrize("N,K,L", [(16, 8, 4), (32, 12, 8), (64, 40, 3), (128, 64, 8), (1024, 512, 8), (2048, 1024, 8),
+                                   (4096, 1400, 4)])
 @pytest.mark.parametrize("kind", KINDS)
 def test_schedule_modes_match_oracle(N, K, L, kind, qpd, oracle_mod, monkeypatch):
     from quantized_decoder_polar_codes_amd import lut as LU
@@ -51,7 +61,7 @@ def test_schedule_modes_match_oracle(N, K, L, kind, qpd, oracle_mod, monkeypatch
     fm, nt = _node_type(N, K)
     if (kind == "FastSC-LUT" and 0 <= nt[0] <= 3) or (kind == "FastSCL-LUT" and 0 <= nt[0] <= 2):
         pytest.skip("special root: rejected on both sides (test_gpu_parity)")
-    B = 40 if N >= 1024 and "SCL" in kind else 150
+    B = (40 if N <= 1024 else 12) if "SCL" in kind else (150 if N <= 1024 else 40)
     sym = np.random.default_rng(N + K + L).integers(0, 16, size=(B, N), dtype=np.int32)
     want = oracle_mod.decode_lut(kind, p, K, L, fm, sym, node_type=nt)
     for env in MODES:
