@@ -257,7 +257,16 @@ __device__ __forceinline__ uint32_t lut_vec(uint32_t T, uint32_t A, uint32_t B, 
 // loads are all issued before the first lookup: the shallow levels live in
 // the global slab, and one memory round trip per chunk instead of per word is
 // what bounds these ops.
-template <bool ISG, int NS>
+// Source word of an f/g op; RAW: S[d] is a slab/LDS row (no channel / pre-pass
+// reads), decided once per op instead of per word.
+template <bool RAW>
+__device__ __forceinline__ uint32_t fg_word(const FastPlan &P, const Mem &M, const MOp &op, const int32_t *y, int src, int w,
+                                            int cnt = 8) {
+    if constexpr (RAW) return M.ld(op.flags & MF_SRC_LDS, op.src_row + w, src);
+    return sym_word(P, M, op, y, src, w, cnt);
+}
+
+template <bool ISG, bool RAW, int NS>
 __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], const MOp &op, const int32_t *const (&y)[NS],
                                       const int (&src)[NS], const int (&usrc)[NS], uint32_t T, int lane) {
     const int ctemp = op.cnt;
@@ -272,8 +281,8 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
                 for (int s = 0; s < NS; ++s) {
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
-                        A[s][k] = sym_word(P, M[s], op, y[s], src[s], w0 + k);
-                        B[s][k] = sym_word(P, M[s], op, y[s], src[s], nwo + w0 + k);
+                        A[s][k] = fg_word<RAW>(P, M[s], op, y[s], src[s], w0 + k);
+                        B[s][k] = fg_word<RAW>(P, M[s], op, y[s], src[s], nwo + w0 + k);
                     }
                     ub[s] = ISG ? M[s].ld(ul, op.u_row + (w0 >> 2), usrc[s]) : 0u;
                 }
@@ -288,8 +297,8 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
                 uint32_t A[8], B[8], ub[2] = {0u, 0u};
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
-                    A[k] = sym_word(P, M[0], op, y[0], src[0], w0 + k);
-                    B[k] = sym_word(P, M[0], op, y[0], src[0], nwo + w0 + k);
+                    A[k] = fg_word<RAW>(P, M[0], op, y[0], src[0], w0 + k);
+                    B[k] = fg_word<RAW>(P, M[0], op, y[0], src[0], nwo + w0 + k);
                 }
                 if (ISG) {
                     ub[0] = M[0].ld(ul, op.u_row + (w0 >> 2), usrc[0]);
@@ -309,8 +318,8 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
             for (int k = 0; k < 4; ++k) {
                 A[s][k] = B[s][k] = 0u;
                 if (k < nwo) {
-                    A[s][k] = sym_word(P, M[s], op, y[s], src[s], k);
-                    B[s][k] = sym_word(P, M[s], op, y[s], src[s], nwo + k);
+                    A[s][k] = fg_word<RAW>(P, M[s], op, y[s], src[s], k);
+                    B[s][k] = fg_word<RAW>(P, M[s], op, y[s], src[s], nwo + k);
                 }
             }
             ub[s] = ISG ? M[s].ld(ul, op.u_row, usrc[s]) : 0u;
@@ -324,7 +333,7 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
         uint32_t W[NS], ub[NS];
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            W[s] = sym_word(P, M[s], op, y[s], src[s], 0, 2 * ctemp);
+            W[s] = fg_word<RAW>(P, M[s], op, y[s], src[s], 0, 2 * ctemp);
             ub[s] = ISG ? M[s].ld(ul, op.u_row, usrc[s]) : 0u;
         }
 #pragma unroll
@@ -1070,10 +1079,15 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QP
                     }
                     if (fl & MF_GSEL)
                         gsel_op(Mv, op, yv, usrc, lane);
-                    else if (op.type == OP_F)
-                        fg_op<false>(P, Mv, op, yv, src, usrc, cur.T, lane);
+                    else if (NS == 2 && !(fl & (MF_CHAN | MF_PRE))) {  // (one-set FastSCL: smaller code measured faster)
+                        if (op.type == OP_F)
+                            fg_op<false, true>(P, Mv, op, yv, src, usrc, cur.T, lane);
+                        else
+                            fg_op<true, true>(P, Mv, op, yv, src, usrc, cur.T, lane);
+                    } else if (op.type == OP_F)
+                        fg_op<false, false>(P, Mv, op, yv, src, usrc, cur.T, lane);
                     else
-                        fg_op<true>(P, Mv, op, yv, src, usrc, cur.T, lane);
+                        fg_op<true, false>(P, Mv, op, yv, src, usrc, cur.T, lane);
 #pragma unroll
                     for (int s = 0; s < NS; ++s) stv[s].ps = pset(stv[s].ps, op.sh_dst, gl);
                     break;
