@@ -259,18 +259,19 @@ __device__ __forceinline__ uint32_t lut_vec(uint32_t T, uint32_t A, uint32_t B, 
 // what bounds these ops.
 // Source word of an f/g op; RAW: S[d] is a slab/LDS row (no channel / pre-pass
 // reads), decided once per op instead of per word.
-template <bool RAW>
+// SL >= 0: the row space of S[d] fixed at compile time (0 slab, 1 LDS).
+template <bool RAW, int SL = -1>
 __device__ __forceinline__ uint32_t fg_word(const FastPlan &P, const Mem &M, const MOp &op, const int32_t *y, int src, int w,
                                             int cnt = 8) {
-    if constexpr (RAW) return M.ld(op.flags & MF_SRC_LDS, op.src_row + w, src);
+    if constexpr (RAW) return M.ld(SL >= 0 ? SL != 0 : (op.flags & MF_SRC_LDS) != 0, op.src_row + w, src);
     return sym_word(P, M, op, y, src, w, cnt);
 }
 
-template <bool ISG, bool RAW, int NS>
+template <bool ISG, bool RAW, int NS, int SL = -1, int DL = -1>
 __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], const MOp &op, const int32_t *const (&y)[NS],
                                       const int (&src)[NS], const int (&usrc)[NS], uint32_t T, int lane) {
     const int ctemp = op.cnt;
-    const bool dl = op.flags & MF_DST_LDS, ul = op.flags & MF_U_LDS;
+    const bool dl = DL >= 0 ? DL != 0 : (op.flags & MF_DST_LDS) != 0, ul = op.flags & MF_U_LDS;
     if (ctemp >= 64) {
         const int nwo = ctemp >> 3;  // multiple of 8
         if constexpr (NS == 2) {
@@ -281,8 +282,8 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
                 for (int s = 0; s < NS; ++s) {
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
-                        A[s][k] = fg_word<RAW>(P, M[s], op, y[s], src[s], w0 + k);
-                        B[s][k] = fg_word<RAW>(P, M[s], op, y[s], src[s], nwo + w0 + k);
+                        A[s][k] = fg_word<RAW, SL>(P, M[s], op, y[s], src[s], w0 + k);
+                        B[s][k] = fg_word<RAW, SL>(P, M[s], op, y[s], src[s], nwo + w0 + k);
                     }
                     ub[s] = ISG ? M[s].ld(ul, op.u_row + (w0 >> 2), usrc[s]) : 0u;
                 }
@@ -297,8 +298,8 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
                 uint32_t A[8], B[8], ub[2] = {0u, 0u};
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
-                    A[k] = fg_word<RAW>(P, M[0], op, y[0], src[0], w0 + k);
-                    B[k] = fg_word<RAW>(P, M[0], op, y[0], src[0], nwo + w0 + k);
+                    A[k] = fg_word<RAW, SL>(P, M[0], op, y[0], src[0], w0 + k);
+                    B[k] = fg_word<RAW, SL>(P, M[0], op, y[0], src[0], nwo + w0 + k);
                 }
                 if (ISG) {
                     ub[0] = M[0].ld(ul, op.u_row + (w0 >> 2), usrc[0]);
@@ -318,8 +319,8 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
             for (int k = 0; k < 4; ++k) {
                 A[s][k] = B[s][k] = 0u;
                 if (k < nwo) {
-                    A[s][k] = fg_word<RAW>(P, M[s], op, y[s], src[s], k);
-                    B[s][k] = fg_word<RAW>(P, M[s], op, y[s], src[s], nwo + k);
+                    A[s][k] = fg_word<RAW, SL>(P, M[s], op, y[s], src[s], k);
+                    B[s][k] = fg_word<RAW, SL>(P, M[s], op, y[s], src[s], nwo + k);
                 }
             }
             ub[s] = ISG ? M[s].ld(ul, op.u_row, usrc[s]) : 0u;
@@ -333,7 +334,7 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
         uint32_t W[NS], ub[NS];
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            W[s] = fg_word<RAW>(P, M[s], op, y[s], src[s], 0, 2 * ctemp);
+            W[s] = fg_word<RAW, SL>(P, M[s], op, y[s], src[s], 0, 2 * ctemp);
             ub[s] = ISG ? M[s].ld(ul, op.u_row, usrc[s]) : 0u;
         }
 #pragma unroll
@@ -1080,10 +1081,21 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QP
                     if (fl & MF_GSEL)
                         gsel_op(Mv, op, yv, usrc, lane);
                     else if (NS == 2 && !(fl & (MF_CHAN | MF_PRE))) {  // (one-set FastSCL: smaller code measured faster)
-                        if (op.type == OP_F)
-                            fg_op<false, true>(P, Mv, op, yv, src, usrc, cur.T, lane);
-                        else
-                            fg_op<true, true>(P, Mv, op, yv, src, usrc, cur.T, lane);
+                        // row spaces of source and destination fixed per instantiation
+                        const int key = ((fl & MF_SRC_LDS) ? 1 : 0) | ((fl & MF_DST_LDS) ? 2 : 0);
+#define QPD_FG(G, S_, D_) fg_op<G, true, NS, S_, D_>(P, Mv, op, yv, src, usrc, cur.T, lane)
+                        if (op.type == OP_F) {
+                            if (key == 0) QPD_FG(false, 0, 0);
+                            else if (key == 1) QPD_FG(false, 1, 0);
+                            else if (key == 2) QPD_FG(false, 0, 1);
+                            else QPD_FG(false, 1, 1);
+                        } else {
+                            if (key == 0) QPD_FG(true, 0, 0);
+                            else if (key == 1) QPD_FG(true, 1, 0);
+                            else if (key == 2) QPD_FG(true, 0, 1);
+                            else QPD_FG(true, 1, 1);
+                        }
+#undef QPD_FG
                     } else if (op.type == OP_F)
                         fg_op<false, false>(P, Mv, op, yv, src, usrc, cur.T, lane);
                     else
