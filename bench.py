@@ -8,13 +8,26 @@ already resident in HBM.  The workload is the reference driver's
 generator (qpd_mc_frames: Philox4x32-10 keyed by global frame id, polar
 encoding, BPSK + AWGN at Eb/N0, LLR), the MinDistortion channel quantizer
 designed at that Eb/N0, and MinDistortion decoder tables designed at 3 dB
-(lutgen.py, the reference generator's algorithm).  With --gpus N>1 the driver runs this under
-torch.distributed.run; every rank decodes its own disjoint frame range (weak
-scaling, no collective on the data path) and the only collective is the RCCL
-all-reduce of the error counters {bit errors, block errors, frames}.
+(lutgen.py, the reference generator's algorithm).
+
+Multi-GPU: one process per GPU.  `--gpus N` with N > 1 and
+no WORLD_SIZE in the environment re-launches this script under
+`torch.distributed.run` (a child process; nothing here has touched the GPU
+yet), so `python bench.py --gpus 8` and the driver's own torchrun launch run
+the same per-rank body (`run_rank`): rank r decodes global frames
+[r*F, (r+1)*F) of one Philox stream (weak scaling, no collective on the data
+path) and the only collectives are the RCCL all-reduces of the error counters
+{bit errors, block errors, frames} and of the timed wall (max over ranks).
+
+`--mc-frames F` runs BASELINE config 5 instead: a Monte-Carlo point of F
+frames (default no early stop, the driver's MaxBlock branch; `--mc-stop 1000`
+= its `Nblkerrs > 1000` rule, mainQuantizedDecoder_LLRDomain.py:130-203)
+sharded over the ranks by global frame id (montecarlo.run_point), and reports
+BER/BLER plus the end-to-end rate (generate + decode + count).
 
 Rank 0 prints one JSON line (contract in the task statement), including
-`roofline` for the decode kernel (HIP-event timing on the launch stream) and
+`roofline` for the decode kernel (HIP events around each of its launches on
+the launch stream; on-chip bytes against the LDS peak probed on this GPU) and
 `cpu_baseline` (the reference decoder compiled from its sources, oracle/_ref,
 one worker process per host core of this GPU's CPU share, over a bounded
 sample of the same frames).
@@ -24,6 +37,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,18 +48,18 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-LDS_PEAK_GBS = 150000.0  # MI355X_MICROARCH.md §LDS: ds_read_b64/b128 aggregate, every CU streaming
 LOOKUPS_PER_FRAME = 81920  # L*N*log2(N) LUT lookups at N=1024, L=8
-ONCHIP_BYTES_PER_LOOKUP = 4
+ONCHIP_BYTES_PER_LOOKUP = 4  # 2 operand symbols + 1 table byte + 1 result byte
+METRIC = "decoded frames/sec (N=1024, SCL-LUT L=8, Q=16) at 1/2/4/8 GPUs; BER match"
+KINDS = ["SC-LUT", "SCL-LUT", "FastSC-LUT", "FastSCL-LUT", "CA-SCL-LUT", "CA-FastSCL-LUT"]
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--kind", default="SCL-LUT", choices=["SC-LUT", "SCL-LUT", "FastSC-LUT", "FastSCL-LUT", "CA-SCL-LUT",
-                                                          "CA-FastSCL-LUT"])
+    ap.add_argument("--kind", default="SCL-LUT", choices=KINDS)
     ap.add_argument("--N", type=int, default=1024)
     ap.add_argument("--K", type=int, default=512)
     ap.add_argument("--L", type=int, default=8)
@@ -53,17 +68,56 @@ def parse():
     ap.add_argument("--max-waves", type=int, default=0)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the generate+decode+count rate")
     ap.add_argument("--engine", default="auto", choices=["auto", "fast", "generic"])
     ap.add_argument("--luts", default="mindistortion", choices=["mindistortion", "minsum"],
                     help="decoder tables: MinDistortion design (lutgen.py) or synthetic saturating min-sum")
     ap.add_argument("--design-snr", type=float, default=3.0, help="LUT design SNR (dB)")
     ap.add_argument("--cpu-workers", type=int, default=0, help="0 = this GPU's CPU share (OMP_NUM_THREADS, <= 16)")
-    return ap.parse_args()
+    ap.add_argument("--mc-frames", type=float, default=0,
+                    help="Monte-Carlo mode (BASELINE config 5): frames of one Eb/N0 point over all ranks, e.g. 1e8")
+    ap.add_argument("--mc-stop", type=int, default=0,
+                    help="Monte-Carlo early stop: Nblkerrs > this (the driver uses 1000); 0 = run all frames")
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------
+# launch
+# ---------------------------------------------------------------------------
+
+def launch_cmd(args, argv, port):
+    """The torch.distributed.run command that runs this script on args.gpus ranks."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def self_launch(args, argv) -> int:
+    """Run the N-rank job as a child process (this process never touches the GPU)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool
+    return subprocess.call(launch_cmd(args, argv, port), env=env)
+
+
+# ---------------------------------------------------------------------------
+# workload
+# ---------------------------------------------------------------------------
+
+class Workload:
+    """This rank's decoder and frames: dec (decode_batch/info/out_bits), the
+    frame source src(frame0, B) -> (msg, sym), packed tables, frozen mask and
+    node types (for the CPU baseline), and this rank's resident batch."""
+
+    def __init__(self, dec, src, packed, fm, nt, msg, sym, frame0):
+        self.dec, self.src, self.packed, self.fm, self.nt = dec, src, packed, fm, nt
+        self.msg, self.sym, self.frame0 = msg, sym, frame0
 
 
 def workload(N, K, L, kind, frames, ebn0, luts="mindistortion", design_snr=3.0, frame0=0, device=None, **dec_kw):
-    """The benchmark workload: (decoder, packed tables, frozen mask, node types,
-    device msg uint8 [F, K], device symbols int32 [F, N]) -- see the module doc."""
+    """The benchmark workload (see the module doc)."""
     import quantized_decoder_polar_codes_amd as Q
     from quantized_decoder_polar_codes_amd import codes as C
     from quantized_decoder_polar_codes_amd import lut as LU
@@ -83,8 +137,248 @@ def workload(N, K, L, kind, frames, ebn0, luts="mindistortion", design_snr=3.0, 
         dec_kw.setdefault("A", K - 24)
     dec = Q.from_packed(kind, packed, K, fm, L=L, node_type=nt, device=device, **dec_kw)
     src = MC.GpuFrames(dec, edges, clut, 16, sigma, seed=1234)  # Philox keyed by global frame id
-    msg, sym = src(frame0, frames)
-    return dec, packed, fm, nt, msg, sym
+    msg, sym = src(frame0, frames) if frames else (None, None)
+    return Workload(dec, src, packed, fm, nt, msg, sym, frame0)
+
+
+# ---------------------------------------------------------------------------
+# the per-rank body
+# ---------------------------------------------------------------------------
+
+class Ctx:
+    """Where this rank runs: device, process group (None = single process) and
+    the device synchronisation (a no-op on CPU, for the gloo tests)."""
+
+    def __init__(self, rank, world, device, group=None):
+        import torch
+
+        self.rank, self.world, self.device, self.group = rank, world, device, group
+        self._cuda = device.type == "cuda"
+        self._torch = torch
+
+    def sync(self):
+        if self._cuda:
+            self._torch.cuda.synchronize(self.device)
+
+    def barrier(self):
+        self.sync()
+        if self.group is not None:
+            import torch.distributed as dist
+
+            dist.barrier(group=self.group)
+        self.sync()
+
+    def allreduce(self, t, op):
+        if self.group is not None:
+            import torch.distributed as dist
+
+            dist.all_reduce(t, op=op, group=self.group)
+        return t
+
+
+def timed_steps(ctx, fn, steps, warmup):
+    """W untimed calls of fn, then exactly `steps` calls bracketed by a barrier
+    and a device sync on both sides; returns (last result, wall seconds)."""
+    out = None
+    for _ in range(warmup):
+        out = fn()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = fn()
+    ctx.barrier()
+    return out, time.perf_counter() - t0
+
+
+def _has_prof(dec):
+    return hasattr(dec, "profile") and hasattr(dec, "kernel_times")
+
+
+def run_rank(args, ctx, wl):
+    """Decode throughput on this rank; returns the result dict on rank 0 (None
+    elsewhere).  Counters and the wall are all-reduced over ctx.group."""
+    import torch
+    import torch.distributed as dist
+
+    dec = wl.dec
+    prof = _has_prof(dec) and ctx._cuda
+    if prof:
+        dec.profile(True)
+    out, wall = timed_steps(ctx, lambda: dec.decode_batch(wl.sym), args.steps, args.warmup)
+    kt = dec.kernel_times() if prof else {}
+    if prof:
+        dec.profile(False)
+
+    # error counters (BER/BLER) -- the only collectives: RCCL all-reduces
+    err = (out != wl.msg)
+    cnt = torch.tensor([int(err.sum().item()), int(err.any(1).sum().item()), int(wl.sym.shape[0])],
+                       dtype=torch.int64, device=ctx.device)
+    tmax = torch.tensor([wall], dtype=torch.float64, device=ctx.device)
+    ctx.allreduce(cnt, dist.ReduceOp.SUM)
+    ctx.allreduce(tmax, dist.ReduceOp.MAX)
+    wall = float(tmax.item())
+    bit_errs, blk_errs, frames_all = (int(x) for x in cnt.tolist())
+    if ctx.rank != 0:
+        return None
+    frames = int(wl.sym.shape[0])
+    res = {
+        "metric": METRIC,
+        "value": frames_all * args.steps / wall,
+        "unit": "frames/s",
+        "n_gpus": ctx.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": ("synthetic, generated on the GPU by qpd_mc_frames (Philox4x32-10 keyed by global frame id): random "
+                 "messages, polar-encoded, BPSK + AWGN at Eb/N0 below, the driver's MinDistortion channel quantizer "
+                 f"(128 -> 16 levels); decoder tables: {args.luts}"
+                 + (f" designed at {args.design_snr:g} dB by lutgen.py" if args.luts == "mindistortion" else "")
+                 + "; resident in HBM"),
+        "config": {"workload": f"{args.kind} N={args.N} K={args.K} L={args.L} Q=16 (5G-NR PW code, no CRC)",
+                   "decoder": args.kind, "N": args.N, "K": args.K, "L": args.L, "v": 16,
+                   "frames_per_gpu_per_step": frames, "ebn0_db": args.ebn0, "luts": args.luts,
+                   "parallelism": f"dp{ctx.world} (frames sharded by global frame id, RCCL counter all-reduce)"},
+        "ber": bit_errs / max(1, frames_all * dec.out_bits),
+        "bler": blk_errs / max(1, frames_all),
+        "frames_counted": frames_all,
+    }
+    if hasattr(dec, "info"):
+        info = dec.info()
+        res["config"].update({"engine": {1: "generic", 2: "fast"}[info["engine"]],
+                              "lds_bytes_per_wave": info["lds_bytes_per_wave"],
+                              "lds_from_depth": info["lds_from_depth"],
+                              "waves": min(info["max_waves"], -(-frames // info["frames_per_wave"]))})
+    if kt:
+        res["roofline"] = roofline(args, dec, kt, frames)
+    return res
+
+
+def _counters(args, frames):
+    """profiles/counters.json record of this configuration (tools/counters.py)."""
+    path = os.path.join(ROOT, "profiles", "counters.json")
+    try:
+        return json.load(open(path)).get(f"{args.kind}_N{args.N}_K{args.K}_L{args.L}_F{frames}")
+    except Exception:
+        return None
+
+
+def roofline(args, dec, kt, frames):
+    """Roofline of the dominant kernel (lut_fast_kernel; generic_decode_kernel
+    on the generic engine).  achieved = SURVEY.md §8(d)'s algorithmic on-chip
+    bytes (L*N*log2 N LUT lookups x 4 B per frame) x frames per launch / the
+    kernel's average launch duration from the HIP events on its stream; peak =
+    the ds_bpermute_b32 rate probed on this GPU now (qpd_probe_lds: the
+    instruction of every table lookup).  `hbm` keeps the contract's HBM view of
+    a whole decode call (pre-pass + decode)."""
+    import ctypes
+
+    from quantized_decoder_polar_codes_amd import _lib
+
+    dec_ms, n_dec = kt["decode"]
+    pre_ms, n_pre = kt["pre"]
+    k_ms = dec_ms / max(1, n_dec)
+    call_ms = (dec_ms + pre_ms) / max(1, n_dec)
+    n = int(np.log2(args.N))
+    onchip_per_frame = args.L * args.N * n * ONCHIP_BYTES_PER_LOOKUP if "SCL" in args.kind else args.N * n * 4
+    peaks = {}
+    for name, op in (("ds_bpermute_b32", _lib.QPD_PROBE_BPERMUTE), ("ds_read_b32", _lib.QPD_PROBE_READ_B32),
+                     ("ds_read_b64", _lib.QPD_PROBE_READ_B64)):
+        g = ctypes.c_double()
+        _lib.check(_lib.load().qpd_probe_lds(dec.device, op, ctypes.byref(g)))
+        peaks[name] = g.value
+    peak = peaks["ds_bpermute_b32"]
+    achieved = onchip_per_frame * frames / (k_ms * 1e-3) / 1e9
+    hbm_bytes = frames * (args.N * 4 + dec.out_bits)  # int32 symbols in, uint8 bits out
+    rec = _counters(args, frames)
+    kname = "lut_fast_kernel" if dec.info()["engine"] == 2 else "generic_decode_kernel"
+    kc = (rec or {}).get("kernels", {}).get(kname, {})
+    out = {"bound": "lds", "achieved": achieved, "peak": peak, "unit": "GB/s", "frac": achieved / peak,
+           "traffic": kc.get("traffic"), "kernel": kname, "kernel_ms": k_ms, "launches": n_dec,
+           "algorithmic_bytes_per_launch": onchip_per_frame * frames,
+           "algorithmic": f"{onchip_per_frame} B/frame on-chip (SURVEY.md §8(d)) x {frames} frames per launch",
+           "peak_probe": peaks, "lds_hit": kc.get("lds_hit"),
+           "traffic_note": "HBM-side bytes per launch of this kernel, 2 x FETCH_SIZE + WRITE_SIZE from separate "
+                           "rocprofv3 --pmc passes (profiles/counters.json via tools/counters.py)",
+           "hbm": {"achieved": hbm_bytes / (call_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": hbm_bytes / (call_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "call_ms": call_ms,
+                   "pre_kernel_ms": pre_ms / max(1, n_pre), "algorithmic_bytes_per_call": hbm_bytes,
+                   "traffic": (kc.get("traffic") or 0) + ((rec or {}).get("kernels", {}).get("root_pre_kernel", {})
+                                                          .get("traffic") or 0) or None}}
+    return out
+
+
+def e2e_rate(args, ctx, wl):
+    """Monte-Carlo rate of generate + decode + count over this rank's next
+    frames (one step = args.frames new frames), all-reduced like run_rank."""
+    import torch
+    import torch.distributed as dist
+
+    dec, src = wl.dec, wl.src
+    prof = _has_prof(dec) and ctx._cuda
+    state = {"f0": wl.frame0 + (1 << 40)}  # frames never decoded by the throughput loop
+    acc = torch.zeros(2, dtype=torch.int64, device=ctx.device)
+
+    def step():
+        msg, sym = src(state["f0"], args.frames)
+        state["f0"] += args.frames
+        e = (dec.decode_batch(sym) != msg).sum(1)
+        acc[0] += e.sum()
+        acc[1] += (e > 0).sum()
+
+    if prof:
+        dec.profile(True)
+    _, wall = timed_steps(ctx, step, args.steps, 1)
+    kt = dec.kernel_times() if prof else {}
+    if prof:
+        dec.profile(False)
+    tmax = torch.tensor([wall], dtype=torch.float64, device=ctx.device)
+    ctx.allreduce(tmax, dist.ReduceOp.MAX)
+    frames = args.frames * args.steps * ctx.world
+    r = {"value": frames / float(tmax.item()), "unit": "frames/s", "ms_per_step": float(tmax.item()) / args.steps * 1e3,
+         "what": "per step: qpd_mc_frames (Philox msg, encode, BPSK+AWGN, channel quantizer) + decode + error count"}
+    if kt:
+        mc_ms, n_mc = kt["mc"]
+        r["mc_kernel_ms"] = mc_ms / max(1, n_mc)
+        r["mc_kernel_bytes"] = args.frames * (args.N * 4 + dec.out_bits)
+        r["mc_kernel_gbs"] = r["mc_kernel_bytes"] / (r["mc_kernel_ms"] * 1e-3) / 1e9
+    return r
+
+
+def mc_rank(args, ctx, wl):
+    """BASELINE config 5: one Monte-Carlo point of args.mc_frames frames sharded
+    over the ranks (montecarlo.run_point; counters all-reduced over RCCL)."""
+    import torch
+    import torch.distributed as dist
+
+    from quantized_decoder_polar_codes_amd import montecarlo as MC
+
+    F = int(args.mc_frames)
+    stop = args.mc_stop if args.mc_stop > 0 else None
+    dec = wl.dec
+    ctx.barrier()
+    t0 = time.perf_counter()
+    r = MC.run_point(wl.src, dec.decode_batch, dec.K, args.ebn0, args.frames, F, stop, A=dec.out_bits,
+                     group=ctx.group, count_device=ctx.device)
+    ctx.barrier()
+    tmax = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=ctx.device)
+    ctx.allreduce(tmax, dist.ReduceOp.MAX)
+    wall = float(tmax.item())
+    if ctx.rank != 0:
+        return None
+    return {"metric": "Monte-Carlo frames/sec (generate + decode + count), N=1024 SCL-LUT L=8 Q=16; BER/BLER",
+            "value": r.frames_decoded / wall, "unit": "frames/s", "n_gpus": ctx.world, "higher_is_better": True,
+            "scaling": "strong", "wall_s": wall, "frames_decoded": r.frames_decoded, "blocks": r.blocks,
+            "ber": r.ber, "bler": r.bler, "bit_errors": r.bit_errors, "block_errors": r.block_errors,
+            "stopped_early": r.stopped_early, "dtype": "u8", "data": "synthetic (qpd_mc_frames, Philox keyed by "
+            "global frame id: identical frames and counters at any rank count)",
+            "config": {"workload": f"{args.kind} N={args.N} K={args.K} L={args.L} Q=16 Monte-Carlo point",
+                       "ebn0_db": args.ebn0, "mc_frames": F, "stop_rule": f"Nblkerrs > {stop}" if stop else "none "
+                       "(MaxBlock branch)", "batch_per_rank": args.frames, "luts": args.luts,
+                       "parallelism": f"dp{ctx.world} (frames sharded by global frame id, RCCL counter all-reduce)"}}
 
 
 _WORKER = r"""
@@ -127,7 +421,7 @@ def cpu_baseline(args, packed, fm, nt, sym, seconds, workers, A):
     the oracle restatement, kind "port", if that build is absent), one worker
     process per core, each decoding its own slice of the sample one frame per
     decode() call for `seconds`.  Workers are plain child processes (no GPU)."""
-    import subprocess
+    import shutil
     import tempfile
 
     per = len(sym) // workers
@@ -150,8 +444,6 @@ def cpu_baseline(args, packed, fm, nt, sym, seconds, workers, A):
         walls.append(r["seconds"])
         kind = r["kind"]
         outs.append((w * per, np.load(path + ".out.npy")))
-    import shutil
-
     shutil.rmtree(tmp, ignore_errors=True)
     wall = max(walls)
     return {"value": total / wall, "unit": "frames/s", "cores": workers, "kind": kind,
@@ -159,121 +451,57 @@ def cpu_baseline(args, packed, fm, nt, sym, seconds, workers, A):
                       f"one decode() call per frame, {wall:.1f} s"}, outs
 
 
-def main():
-    args = parse()
+def rank_job(args, ctx, make_workload):
+    """Everything one rank runs: its workload (global frames [r*F, (r+1)*F) of
+    one Philox stream), then the throughput steps and the end-to-end rate, or
+    the Monte-Carlo point.  Returns (rank 0's result dict or None, workload)."""
+    wl = make_workload(ctx.rank * args.frames, 0 if args.mc_frames else args.frames)
+    ctx.sync()
+    if args.mc_frames:
+        return mc_rank(args, ctx, wl), wl
+    res = run_rank(args, ctx, wl)
+    if not args.no_e2e:
+        e2e = e2e_rate(args, ctx, wl)
+        if res is not None:
+            res["monte_carlo_e2e"] = e2e
+    return res, wl
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args, argv))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local if world > 1 else 0)
+    group = None
     if world > 1:
-        torch.cuda.set_device(local)
         dist.init_process_group("nccl")  # RCCL over xGMI
-    else:
-        torch.cuda.set_device(0)
+        group = dist.group.WORLD
     dev = torch.device("cuda", torch.cuda.current_device())
+    ctx = Ctx(rank, world, dev, group)
 
-    N, K, L = args.N, args.K, args.L
-    # rank r owns global frames [r*F, (r+1)*F) of one Philox stream
-    dec, packed, fm, nt, d_msg, d_sym = workload(N, K, L, args.kind, args.frames, args.ebn0, args.luts, args.design_snr,
-                                                 frame0=rank * args.frames, device=dev.index,
-                                                 max_waves=args.max_waves, engine=args.engine)
-    info = dec.info()
-    torch.cuda.synchronize()
-    stream = torch.cuda.current_stream(dev)
+    def make(frame0, frames):
+        return workload(args.N, args.K, args.L, args.kind, frames, args.ebn0, args.luts, args.design_snr,
+                        frame0=frame0, device=dev.index, max_waves=args.max_waves, engine=args.engine)
 
-    out = None
-    for _ in range(args.warmup):
-        out = dec.decode_batch(d_sym)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        out = dec.decode_batch(d_sym)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / max(1, args.steps)  # kernel launches on this stream, per step
-
-    # error counters (BER/BLER) -- the only collective: RCCL all-reduce
-    err = (out != d_msg)
-    cnt = torch.tensor([int(err.sum().item()), int(err.any(1).sum().item()), args.frames], dtype=torch.int64, device=dev)
-    tmax = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    wall = float(tmax.item())
-    bit_errs, blk_errs, frames_all = (int(x) for x in cnt.tolist())
-    total_frames = args.frames * world * args.steps
-    value = total_frames / wall
-
-    if rank == 0:
-        frames_per_launch = args.frames
-        hbm_bytes = frames_per_launch * (N * 4 + K)  # int32 symbols in, uint8 bits out
-        achieved = hbm_bytes / (kern_ms * 1e-3) / 1e9
-        onchip = frames_per_launch * LOOKUPS_PER_FRAME * ONCHIP_BYTES_PER_LOOKUP * (L / 8) * (N / 1024) \
-            / (kern_ms * 1e-3) / 1e9
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            try:
-                rec = json.load(open(pmc))
-                key = f"{args.kind}_N{N}_K{K}_L{L}_F{frames_per_launch}"
-                traffic = rec.get(key)
-            except Exception:
-                traffic = None
-        res = {
-            "metric": "decoded frames/sec (N=1024, SCL-LUT L=8, Q=16) at 1/2/4/8 GPUs; BER match",
-            "value": value,
-            "unit": "frames/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": wall / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": ("synthetic, generated on the GPU by qpd_mc_frames (Philox4x32-10 keyed by global frame id): random "
-                     "messages, polar-encoded, BPSK + AWGN at Eb/N0 below, the driver's MinDistortion channel quantizer "
-                     f"(128 -> 16 levels); decoder tables: {args.luts}"
-                     + (f" designed at {args.design_snr:g} dB by lutgen.py" if args.luts == "mindistortion" else "")
-                     + "; resident in HBM"),
-            "config": {"workload": f"{args.kind} N={N} K={K} L={L} Q=16 (5G-NR PW code, no CRC)",
-                       "decoder": args.kind, "N": N, "K": K, "L": L, "v": 16, "frames_per_gpu_per_step": args.frames,
-                       "ebn0_db": args.ebn0, "luts": args.luts, "parallelism": f"dp{world} (frames sharded, RCCL counter all-reduce)",
-                       "engine": {1: "generic", 2: "fast"}[info["engine"]], "lds_bytes_per_wave": info["lds_bytes_per_wave"],
-                       "lds_from_depth": info["lds_from_depth"], "waves": min(info["max_waves"],
-                       -(-args.frames // info["frames_per_wave"]))},
-            "ber": bit_errs / max(1, frames_all * dec.out_bits),
-            "bler": blk_errs / max(1, frames_all),
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": hbm_bytes,
-                         "kernels": "one decode call = root_pre_kernel + lut_fast_kernel on the bench stream "
-                                    "(HIP events bracket both; traffic sums both)" if info["engine"] == 2 else
-                                    "generic_decode_kernel",
-                         "onchip_lds_equiv": {"achieved": onchip, "peak": LDS_PEAK_GBS, "unit": "GB/s",
-                                              "frac": onchip / LDS_PEAK_GBS,
-                                              "bytes_per_frame": LOOKUPS_PER_FRAME * ONCHIP_BYTES_PER_LOOKUP}},
-        }
-        if world == 1 and not args.no_cpu_baseline:
+    res, wl = rank_job(args, ctx, make)
+    if not args.mc_frames:
+        if res is not None and world == 1 and not args.no_cpu_baseline:
             workers = args.cpu_workers or min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
-            sample = d_sym[: 1 << 15].cpu().numpy()
-            cb, parts = cpu_baseline(args, packed, fm, nt, sample, args.cpu_baseline_seconds, max(1, workers),
-                                     dec.out_bits)
+            sample = wl.sym[: 1 << 15].cpu().numpy()
+            cb, parts = cpu_baseline(args, wl.packed, wl.fm, wl.nt, sample, args.cpu_baseline_seconds,
+                                     max(1, workers), wl.dec.out_bits)
             res["cpu_baseline"] = cb
-            gpu_out = out.cpu().numpy()
+            gpu_out = wl.dec.decode_batch(wl.sym[: 1 << 15]).cpu().numpy()
             ok = all(np.array_equal(gpu_out[o:o + len(r)], r) for o, r in parts)
             res["parity_sample"] = {"frames": int(sum(len(r) for _, r in parts)), "bit_exact_vs_" + cb["kind"]: bool(ok)}
+    if res is not None:
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

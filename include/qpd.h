@@ -257,6 +257,34 @@ typedef struct qpd_info {
 } qpd_info;
 int qpd_get_info(const qpd_decoder *dec, qpd_info *info);
 
+/*
+ * Kernel timing for benchmarks (no reference counterpart).  While enabled,
+ * every kernel launch of this handle is bracketed by HIP events recorded on
+ * the launch stream; qpd_kernel_times waits for them and returns, per kernel
+ * class, the summed durations (ms) and the number of launches since the last
+ * call, then forgets them.  Arrays have QPD_KC_COUNT entries.
+ */
+enum qpd_kernel_class {
+    QPD_KC_PRE = 0,    /* root_pre_kernel (fast engine, root pre-pass)              */
+    QPD_KC_DECODE = 1, /* lut_fast_kernel / generic_decode_kernel                   */
+    QPD_KC_MC = 2,     /* mc_frames_kernel (qpd_mc_frames)                          */
+    QPD_KC_COUNT = 3
+};
+int qpd_profile(qpd_decoder *dec, int32_t enable);
+int qpd_kernel_times(qpd_decoder *dec, double *ms, int64_t *launches);
+
+/*
+ * On-chip peak probe (no reference counterpart): the LDS-path rate of one
+ * instruction with every CU busy, measured on `device` by a streaming
+ * microbenchmark (independent chains, 16 wave-instructions in flight per
+ * wave, 8 waves per CU).  op: QPD_PROBE_BPERMUTE (ds_bpermute_b32, the
+ * decoder's table lookups and fork copies), QPD_PROBE_READ_B32 (ds_read_b32,
+ * its LDS rows), QPD_PROBE_READ_B64.  *gbps = bytes moved (64 lanes x width
+ * per wave-instruction) / s.
+ */
+enum qpd_probe_op { QPD_PROBE_BPERMUTE = 0, QPD_PROBE_READ_B32 = 1, QPD_PROBE_READ_B64 = 2 };
+int qpd_probe_lds(int32_t device, int32_t op, double *gbps);
+
 #ifdef __cplusplus
 }
 #endif

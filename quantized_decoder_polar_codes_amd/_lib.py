@@ -36,7 +36,12 @@ EXPORTED = (
     "qpd_mc_frames",
     "qpd_optls_quantizer",
     "qpd_lutgen_mindistortion",
+    "qpd_profile",
+    "qpd_kernel_times",
+    "qpd_probe_lds",
 )
+QPD_KC_PRE, QPD_KC_DECODE, QPD_KC_MC, QPD_KC_COUNT = range(4)
+QPD_PROBE_BPERMUTE, QPD_PROBE_READ_B32, QPD_PROBE_READ_B64 = range(3)
 
 _P = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -162,6 +167,12 @@ def load():
     L.qpd_optls_quantizer.restype = ctypes.c_int
     L.qpd_lutgen_mindistortion.argtypes = [_i32, _i32, _P, _P, _i32, _i32, _P, _P, _P, _P]
     L.qpd_lutgen_mindistortion.restype = ctypes.c_int
+    L.qpd_profile.argtypes = [_P, _i32]
+    L.qpd_profile.restype = ctypes.c_int
+    L.qpd_kernel_times.argtypes = [_P, _P, _P]
+    L.qpd_kernel_times.restype = ctypes.c_int
+    L.qpd_probe_lds.argtypes = [_i32, _i32, ctypes.POINTER(ctypes.c_double)]
+    L.qpd_probe_lds.restype = ctypes.c_int
     if L.qpd_abi_version() != ABI_VERSION:
         raise ImportError("libqpd.so ABI version mismatch")
     _lib = L

@@ -14,6 +14,7 @@
 #include "qpd_generic.hip"
 #include "qpd_fast.hip"
 #include "qpd_mc.hip"
+#include "qpd_probe.hip"
 
 namespace {
 
@@ -125,6 +126,16 @@ struct qpd_decoder {
     // staging for the host-buffer entry points
     DeviceBuf h_in, h_out;
     size_t h_in_bytes = 0, h_out_bytes = 0;
+    // qpd_profile: HIP events around every launch, per kernel class
+    bool prof = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[QPD_KC_COUNT];
+    ~qpd_decoder() {
+        for (auto &v : prof_ev)
+            for (auto &e : v) {
+                (void)hipEventDestroy(e.first);
+                (void)hipEventDestroy(e.second);
+            }
+    }
 };
 
 namespace {
@@ -140,6 +151,24 @@ int upload(DeviceBuf &b, const T *src, size_t count) {
 int set_device(const qpd_decoder *d) {
     if (d->device >= 0) QPD_HIP(hipSetDevice(d->device));
     return QPD_OK;
+}
+
+// One kernel launch of class kc on stream st; bracketed by HIP events on that
+// stream while profiling is enabled (qpd_profile / qpd_kernel_times).
+template <class F>
+int timed_launch(qpd_decoder *d, int kc, hipStream_t st, F &&launch) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (d->prof) {
+        QPD_HIP(hipEventCreate(&e0));
+        QPD_HIP(hipEventCreate(&e1));
+        QPD_HIP(hipEventRecord(e0, st));
+    }
+    const int rc = launch();
+    if (d->prof) {
+        QPD_HIP(hipEventRecord(e1, st));
+        d->prof_ev[kc].emplace_back(e0, e1);
+    }
+    return rc;
 }
 
 // Kernel family (SC / SCL / FastSC / FastSCL, as the LUT kind ids) and symbol
@@ -695,9 +724,11 @@ int launch_generic(qpd_decoder *d, const In *in, int64_t B, uint8_t *out, int gr
     qpd::DevPlan P = d->plan;
     const In *in_arg = in;
     void *args[] = {&P, &in_arg, &B, &out};
-    QPD_HIP(hipLaunchKernel(kfn, dim3(grid), dim3(64), args, 0, st));
-    QPD_HIP(hipGetLastError());
-    return QPD_OK;
+    return timed_launch(d, QPD_KC_DECODE, st, [&]() -> int {
+        QPD_HIP(hipLaunchKernel(kfn, dim3(grid), dim3(64), args, 0, st));
+        QPD_HIP(hipGetLastError());
+        return QPD_OK;
+    });
 }
 
 }  // namespace
@@ -940,9 +971,11 @@ int qpd_decode(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_o
             fgrid = (int)((fgroups + rounds - 1) / rounds);
             const qpd::MOp *ops_arg = fp.ops;
             void *args[] = {&fp, &in_arg, &Bc, &out_arg, &ops_arg};
-            QPD_HIP(hipLaunchKernel(kfn, dim3(fgrid), dim3(64), args, lds, st));
-            QPD_HIP(hipGetLastError());
-            return QPD_OK;
+            return timed_launch(d, QPD_KC_DECODE, st, [&]() -> int {
+                QPD_HIP(hipLaunchKernel(kfn, dim3(fgrid), dim3(64), args, lds, st));
+                QPD_HIP(hipGetLastError());
+                return QPD_OK;
+            });
         };
         if (!d->pre) {
             fp.in_shift = fp.n;
@@ -964,11 +997,15 @@ int qpd_decode(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_o
             fp.in_shift = fp.n;
             const int pgrid = (int)std::min<int64_t>(((Bc << (fp.n - 4)) + 255) / 256, 8192);
             void *pargs[] = {&fp, &sym, &Bc, &pre};
-            QPD_HIP(hipLaunchKernel(reinterpret_cast<const void *>(&qpd::root_pre_kernel), dim3(pgrid), dim3(256), pargs,
-                                    0, st));
-            QPD_HIP(hipGetLastError());
+            rc = timed_launch(d, QPD_KC_PRE, st, [&]() -> int {
+                QPD_HIP(hipLaunchKernel(reinterpret_cast<const void *>(&qpd::root_pre_kernel), dim3(pgrid), dim3(256),
+                                        pargs, 0, st));
+                QPD_HIP(hipGetLastError());
+                return QPD_OK;
+            });
+            if (rc) return rc;
             fp.in_shift = fp.n - 2;
-            const int rc = decode((const int32_t *)pre, Bc, d_out + f0 * fp.out_k);
+            rc = decode((const int32_t *)pre, Bc, d_out + f0 * fp.out_k);
             if (rc) return rc;
         }
         return QPD_OK;
@@ -1079,9 +1116,44 @@ int qpd_mc_frames(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64
     for (int i = 0; i < ch->n_edges; ++i) C.edges[i] = ch->edges[i];
     for (int i = 0; i + 1 < ch->n_edges; ++i) C.lut[i] = ch->lut[i];
     const int grid = (int)std::min<int64_t>(B, 256 * 16);
-    hipLaunchKernelGGL(qpd::mc_frames_kernel, dim3(grid), dim3(64), (size_t)d->N, (hipStream_t)stream, C, frame0, B,
-                       d_msg, d_symbols);
-    QPD_HIP(hipGetLastError());
+    return timed_launch(d, QPD_KC_MC, (hipStream_t)stream, [&]() -> int {
+        hipLaunchKernelGGL(qpd::mc_frames_kernel, dim3(grid), dim3(64), (size_t)d->N, (hipStream_t)stream, C, frame0, B,
+                           d_msg, d_symbols);
+        QPD_HIP(hipGetLastError());
+        return QPD_OK;
+    });
+}
+
+int qpd_probe_lds(int32_t device, int32_t op, double *gbps) {
+    if (!gbps || op < 0 || op > 2) return fail(QPD_E_INVALID, "bad probe op / null output");
+    if (device >= 0) QPD_HIP(hipSetDevice(device));
+    QPD_HIP(qpd::probe_lds_run(op, gbps));
+    return QPD_OK;
+}
+
+int qpd_profile(qpd_decoder *d, int32_t enable) {
+    if (!d) return fail(QPD_E_INVALID, "null decoder");
+    d->prof = enable != 0;
+    return QPD_OK;
+}
+
+int qpd_kernel_times(qpd_decoder *d, double *ms, int64_t *launches) {
+    if (!d || !ms || !launches) return fail(QPD_E_INVALID, "null argument");
+    int rc = set_device(d);
+    if (rc) return rc;
+    for (int k = 0; k < QPD_KC_COUNT; ++k) {
+        ms[k] = 0.0;
+        launches[k] = (int64_t)d->prof_ev[k].size();
+        for (auto &e : d->prof_ev[k]) {
+            float t = 0.f;
+            QPD_HIP(hipEventSynchronize(e.second));
+            QPD_HIP(hipEventElapsedTime(&t, e.first, e.second));
+            ms[k] += t;
+            QPD_HIP(hipEventDestroy(e.first));
+            QPD_HIP(hipEventDestroy(e.second));
+        }
+        d->prof_ev[k].clear();
+    }
     return QPD_OK;
 }
 

@@ -136,6 +136,19 @@ class _DecoderBase:
         _lib.check(_lib.load().qpd_get_info(self._h, ctypes.byref(inf)))
         return {k: getattr(inf, k) for k, _ in inf._fields_}
 
+    def profile(self, enable: bool = True) -> None:
+        """Bracket every kernel launch of this decoder with HIP events on its
+        stream (qpd_profile); read the sums with :meth:`kernel_times`."""
+        _lib.check(_lib.load().qpd_profile(self._h, int(bool(enable))))
+
+    def kernel_times(self) -> dict:
+        """{class: (ms summed, launches)} since the last call, for the classes
+        'pre' (root pre-pass), 'decode' and 'mc' (frame generator)."""
+        ms = (ctypes.c_double * _lib.QPD_KC_COUNT)()
+        n = (ctypes.c_int64 * _lib.QPD_KC_COUNT)()
+        _lib.check(_lib.load().qpd_kernel_times(self._h, ms, n))
+        return {name: (ms[i], n[i]) for i, name in enumerate(("pre", "decode", "mc"))}
+
     # -- decoding --------------------------------------------------------------
     def _frame(self, x) -> np.ndarray:
         a = np.asarray(x)

@@ -97,17 +97,46 @@ def _frame_errors(bits, msg):
     return (np.asarray(bits) != np.asarray(msg)).sum(axis=1).astype(np.int64)
 
 
-def run_point(generate, decode, K: int, ebn0_db: float, batch: int, max_blocks: int, stop_blkerrs: int = 1000,
+def _run_point_all(generate, decode, K, ebn0_db, batch, max_blocks, world, rank, group, count_device):
+    """run_point without early stop (the driver's MaxBlock branch, :194-196):
+    counters accumulate on the device, one all-reduce at the end."""
+    import torch
+    import torch.distributed as dist
+
+    acc = torch.zeros(2, dtype=torch.int64, device=count_device)
+    f0 = 0
+    while f0 < max_blocks:
+        step = min(world * batch, max_blocks - f0)
+        lo = f0 + min(rank * batch, step)
+        hi = f0 + min((rank + 1) * batch, step)
+        if hi > lo:
+            msg, sym = generate(lo, hi - lo)
+            e = _frame_errors(decode(sym), msg)
+            e_t = (e if isinstance(e, torch.Tensor) else torch.from_numpy(e)).to(count_device)
+            acc[0] += e_t.sum()
+            acc[1] += (e_t > 0).sum()
+        f0 += step
+    if group is not None:
+        dist.all_reduce(acc, group=group)
+    bit_errs, blk_errs = (int(x) for x in acc.tolist())
+    blocks = max_blocks
+    return PointResult(ebn0_db, bit_errs / (K * blocks), blk_errs / blocks, bit_errs, blk_errs, blocks, blocks, False)
+
+
+def run_point(generate, decode, K: int, ebn0_db: float, batch: int, max_blocks: int, stop_blkerrs: int | None = 1000,
               A: int | None = None, group=None, count_device="cpu") -> PointResult:
     """Run one Eb/N0 point.  ``generate(frame0, B) -> (msg, sym)`` and
     ``decode(sym) -> bits`` are this rank's frame source and decoder;
-    ``group`` is a torch.distributed process group (None = single process)."""
+    ``group`` is a torch.distributed process group (None = single process).
+    ``stop_blkerrs=None``: no early stop (every frame up to max_blocks)."""
     import torch
     import torch.distributed as dist
 
     A = K if A is None else A
     world = dist.get_world_size(group) if group is not None else 1
     rank = dist.get_rank(group) if group is not None else 0
+    if stop_blkerrs is None:
+        return _run_point_all(generate, decode, K, ebn0_db, batch, max_blocks, world, rank, group, count_device)
     bit_errs = blk_errs = 0
     blocks = 0
     f0 = 0
