@@ -20,8 +20,9 @@ def pytest_configure(config):
 def golden_files(pattern="*.npz"):
     """Decoder fixtures.  The default pattern gives the LUT and SC decoders'
     fixtures; the LUT-generator (lutgen_*.npz) and float-domain (float_*.npz)
-    fixtures have their own tests and are returned only when asked for."""
-    own = ("lutgen_", "float_")
+    fixtures and the code-construction pin (codes_*.npz) have their own tests
+    and are returned only when asked for."""
+    own = ("lutgen_", "float_", "codes_")
     return sorted(p for p in glob.glob(os.path.join(GOLDEN_DIR, pattern))
                   if pattern.startswith(own) or not os.path.basename(p).startswith(own))
 

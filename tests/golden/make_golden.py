@@ -12,9 +12,9 @@ Frames follow the reference driver's channel model
 (mainQuantizedDecoder_LLRDomain.py:132-176): message bits, polar encoding
 (restated PolarEnc), BPSK, AWGN at Eb/N0 with sigma = sqrt(1/(2 R Eb/N0)),
 LLR = 2y/sigma^2, then a channel quantizer to `v` symbols.  The channel
-quantizer here is uniform (MinDistortion channel design needs the OpenCV
-quantizer module, which the image lacks); decoder parity does not depend on
-how symbols or tables were designed.
+quantizer of the first fixtures is uniform; the `*_mindist` fixtures use the
+BASELINE workloads' MinDistortion tables and channel quantizer (lutgen.py,
+pinned to the reference's own generator by tests/golden/lutgen_*.npz).
 
 Usage:  python tests/golden/make_golden.py      (needs oracle/_ref built)
 """
@@ -131,6 +131,36 @@ def make_ca_case(R, name, kind, N, A, L, lut_kind, B, ebn0, seed, crc_n=24):
     print(f"{name:28s} {kind:14s} N={N} K={K} A={A} L={L} B={B} ref {dt:.1f}s  BLER={(out != msg).any(1).mean():.3f}")
 
 
+def make_md_case(R, name, kind, N, K, L, B, ebn0, seed, design_snr=3.0):
+    """The BASELINE workloads as the driver runs them: MinDistortion decoder
+    tables designed at `design_snr` (lutgen.design -- bit-exact with the
+    reference's own generator, tests/test_lutgen.py) and the driver's
+    MinDistortion channel quantizer at this Eb/N0 (128 uniform bins -> 16,
+    mainQuantizedDecoder_LLRDomain.py:136-176)."""
+    from quantized_decoder_polar_codes_amd import lutgen as LG
+
+    rng = np.random.default_rng(seed)
+    _, msgbits, frozen, msgmask = C.construct_pw(N, K)
+    node_type = C.identify_nodes(N, msgbits).astype(np.int32)
+    packed = LG.design(N, 16, design_snr).packed()
+    sigma = np.sqrt(1 / (2 * (K / N) * 10 ** (ebn0 / 10)))
+    _, _, edges, clut = LG.channel_quantizer(sigma, 128, 16)
+    msg, llr = awgn_llr(rng, N, K, msgbits, B, ebn0)
+    sym = C.quantize_channel(llr, edges, clut, 16)
+    t = time.time()
+    out = ref_decode(R, kind, N, K, L, frozen, msgmask, node_type, packed, sym)
+    dt = time.time() - t
+    np.savez_compressed(
+        os.path.join(HERE, name + ".npz"),
+        kind=kind, N=N, K=K, L=L, v=16, lut_kind="mindistortion", design_snr_db=design_snr, ebn0_db=ebn0, seed=seed,
+        frozen=frozen.astype(np.int8), node_type=node_type.astype(np.int8),
+        lut_f=packed.lut_f, f_base=packed.f_base, f_step=packed.f_step,
+        lut_g=packed.lut_g, g_base=packed.g_base, g_step=packed.g_step,
+        vcl=packed.vcl, channel_edges=edges, channel_lut=clut, msg=msg, symbols=sym.astype(np.uint8), expected=out,
+    )
+    print(f"{name:34s} {kind:12s} N={N} K={K} L={L} B={B} ref {dt:.1f}s  BLER={(out != msg).any(1).mean():.3f}")
+
+
 def make_float_case(R, name, N, K, B, ebn0, seed):
     rng = np.random.default_rng(seed)
     _, msgbits, frozen, msgmask = C.construct_pw(N, K)
@@ -170,9 +200,21 @@ def main_ca():
     make_ca_case(R, "ca_fastscllut_n1024_a488_l8_minsum", "CA-FastSCL-LUT", 1024, 488, 8, "minsum", 150, 1.5, 15)
 
 
+def main_md():
+    R = O.reference_module()
+    if R is None:
+        raise SystemExit("oracle/_ref not built (run oracle/build_ref.sh)")
+    make_md_case(R, "sclut_n128_k32_mindist", "SC-LUT", 128, 32, 1, 2000, 2.0, 21)  # BASELINE config 2
+    make_md_case(R, "scllut_n1024_k512_l8_mindist", "SCL-LUT", 1024, 512, 8, 300, 2.0, 22)  # config 3
+    make_md_case(R, "fastscllut_n1024_k512_l8_mindist", "FastSCL-LUT", 1024, 512, 8, 200, 2.0, 23)  # config 4
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["ca"]:
         main_ca()  # only the CRC-aided fixtures
+    elif sys.argv[1:] == ["md"]:
+        main_md()  # only the MinDistortion (BASELINE workload) fixtures
     else:
         main()
         main_ca()
+        main_md()
