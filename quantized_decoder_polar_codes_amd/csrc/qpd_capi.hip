@@ -110,6 +110,7 @@ struct qpd_decoder {
     int ca_A = 0, crc_n = 0;
     uint32_t crc_q = 0;
     DeviceBuf info_mask;
+    DeviceBuf mc_pref, mc_crc;  // qpd_mc_frames: info bits before each word; CRC contribution per message bit
     int sets = 1;  // fast engine: frame sets per wave (lut_fast_kernel NS)
     bool l8 = false;  // fast engine: list decoder with L = 8 (select_survivors8)
     bool pre = false;         // fast engine pre-mode: root_pre_kernel, then the decode on its rows
@@ -1099,26 +1100,55 @@ int qpd_mc_frames(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64
     }
     int rc = set_device(d);
     if (rc) return rc;
+    if (!d->mc_pref.p) {  // per-decoder constants of the generator, built at the first call
+        const int nw = (d->N + 31) / 32;
+        std::vector<int32_t> pref(nw, 0);
+        std::vector<uint32_t> mask(nw, 0u);
+        QPD_HIP(hipMemcpy(mask.data(), d->info_mask.p, nw * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        for (int w = 1; w < nw; ++w) pref[w] = pref[w - 1] + __builtin_popcount(mask[w - 1]);
+        // CRC register after message bit j and A-1-j zero bits (the register is
+        // linear in the message bits, utils.cpp:77-92): tab[A-1] = taps,
+        // tab[j] = one zero step of tab[j+1]
+        const int A = d->crc_n > 0 ? d->ca_A : 0;
+        std::vector<uint32_t> tab(std::max(A, 1), 0u);
+        if (A > 0) {
+            const uint32_t top = 1u << (d->crc_n - 1), msk = (top << 1) - 1u;
+            tab[A - 1] = d->crc_q & msk;
+            for (int j = A - 2; j >= 0; --j) {
+                const uint32_t r = tab[j + 1];
+                tab[j] = ((r << 1) & msk) ^ ((r & top) ? d->crc_q : 0u);
+            }
+        }
+        int rc2 = upload(d->mc_pref, pref.data(), pref.size());
+        if (rc2) return rc2;
+        rc2 = upload(d->mc_crc, tab.data(), tab.size());
+        if (rc2) return rc2;
+    }
     qpd::McChannel C;
     std::memset(&C, 0, sizeof(C));
     C.N = d->N;
     C.K = d->K;
     C.A = d->crc_n > 0 ? d->ca_A : d->K;
     C.crc_n = d->crc_n;
-    C.crc_q = d->crc_q;
     C.q = ch->q;
     C.n_edges = ch->n_edges;
     C.seed_lo = (uint32_t)seed;
     C.seed_hi = (uint32_t)(seed >> 32);
-    C.sigma = (float)ch->sigma;
-    C.llr_scale = (float)(2.0 / (ch->sigma * ch->sigma));
-    C.info_pos = (const int32_t *)d->info_pos.p;
+    C.sigma = ch->sigma;
+    C.s2 = ch->sigma * ch->sigma;
+    C.info_mask = (const uint32_t *)d->info_mask.p;
+    C.info_pref = (const int32_t *)d->mc_pref.p;
+    C.crc_tab = (const uint32_t *)d->mc_crc.p;
     for (int i = 0; i < ch->n_edges; ++i) C.edges[i] = ch->edges[i];
     for (int i = 0; i + 1 < ch->n_edges; ++i) C.lut[i] = ch->lut[i];
-    const int grid = (int)std::min<int64_t>(B, 256 * 16);
+    int dev = 0, ncu = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int grid = (int)std::min<int64_t>(B, (int64_t)ncu * 32);
+    const size_t lds = qpd::mc_lds_bytes(d->N, d->K);
     return timed_launch(d, QPD_KC_MC, (hipStream_t)stream, [&]() -> int {
-        hipLaunchKernelGGL(qpd::mc_frames_kernel, dim3(grid), dim3(64), (size_t)d->N, (hipStream_t)stream, C, frame0, B,
-                           d_msg, d_symbols);
+        hipLaunchKernelGGL(qpd::mc_frames_kernel, dim3(grid), dim3(64), lds, (hipStream_t)stream, C, frame0, B, d_msg,
+                           d_symbols);
         QPD_HIP(hipGetLastError());
         return QPD_OK;
     });

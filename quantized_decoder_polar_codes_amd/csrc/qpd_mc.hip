@@ -1,16 +1,32 @@
 // qpd_mc.hip -- GPU-resident Monte-Carlo front end.
 //
 // Replaces the reference driver's per-frame Python loop
-// (mainQuantizedDecoder_LLRDomain.py:151-176): message bits, polar encoding
-// (the un-vendored PolarEnc, restated: u[info] = msg, x = u F^{(x)n} in natural
-// order), BPSK, AWGN, LLR = 2y/sigma^2 and the driver's channel quantizer
-// (saturate at the outer edges, else channel_lut[bisect_left(edges[:-1], llr) - 1]).
+// (mainQuantizedDecoder_LLRDomain.py:151-176): message bits, optional CRC
+// (CRCEnc, :153-156), polar encoding (the un-vendored PolarEnc, restated:
+// u[info] = msg, x = u F^{(x)n} in natural order), BPSK, AWGN in float64
+// (`y = bpsk + normal(0, sigma)`, `llr = y * 2 / sigma**2`, :161-165, with the
+// same roundings: no fused multiply-add) and the driver's channel quantizer
+// (saturate at the outer edges, else channel_lut[bisect_left(edges[:-1], llr) - 1],
+// :167-176).
 //
 // Every random number is a pure function of (seed, GLOBAL frame id, word):
 // Philox4x32-10 with counter = (frame_lo, frame_hi, word, stream tag), so a
 // frame's content does not depend on batch size, grid, or how frames are
 // sharded across GPUs -- the 1/2/4/8-GPU runs of one frame range see the same
-// frames.
+// frames.  Gaussians: Box-Muller in float64 on 53-bit
+// uniforms (two Philox words each), u1 in (0, 1], u2 in [0, 1).
+//
+// bisect_left is exact for any ascending edges: the walk from a guess ends at
+// the first edge >= llr whatever the guess (uniform edges, the driver's
+// linspace, need 0-1 steps).
+//
+// Work mapping: one wave per frame (grid-stride).  The frame's bits are
+// handled bit-packed (32 positions per dword): lane d draws message dword d,
+// the CRC is a table XOR (the register is linear in the message bits), the
+// info bits are deposited into u words by the per-word info masks, and the
+// encoder runs 5 in-word butterfly stages as shift/mask XORs plus log2(N/32)
+// word stages in LDS.  Noise, LLR and quantizer: one position pair per lane
+// and round, stored as int2 (512 B per wave-instruction, coalesced).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -48,88 +64,166 @@ __host__ __device__ inline Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint3
 
 struct McChannel {
     int32_t N, K, q, n_edges;
-    int32_t A, crc_n;  // crc_n > 0: A message bits + first K-A bits of their CRC
-    uint32_t crc_q;    // CRC register taps (coefficients 1..crc_n, as ca_winner)
+    int32_t A, crc_n;     // crc_n > 0: A message bits + first K-A bits of their CRC
+    double sigma, s2;     // AWGN std and sigma*sigma (the driver's sigma ** 2)
     uint32_t seed_lo, seed_hi;
-    float sigma, llr_scale;  // AWGN std and 2/sigma^2
-    const int32_t *info_pos; // [K] information positions, ascending
-    double edges[kMcMaxEdges];
+    const uint32_t *info_mask;  // [N/32] bit i of word w: position 32w+i is an information bit
+    const int32_t *info_pref;   // [N/32] information bits before word w
+    const uint32_t *crc_tab;    // [A] CRC register contribution of message bit j (CA kinds)
+    double edges[kMcMaxEdges];  // [n_edges], ascending (kernel arguments; staged in LDS)
     int32_t lut[kMcMaxEdges - 1];
 };
 
-// One 64-lane workgroup per frame (grid-stride).  LDS: N bytes of u / x.
+// 53-bit uniform from two Philox words: k = (a >> 5) * 2^26 + (b >> 6), k * 2^-53.
+__device__ __host__ inline uint64_t mc_u53(uint32_t a, uint32_t b) {
+    return ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
+}
+
+// sin and cos of x in [0, 2 pi] for the Box-Muller angle: reduction by
+// q = rint(x * 2/pi) against pi/2 in three parts (Cody-Waite), then the
+// fdlibm kernel polynomials (__kernel_sin / __kernel_cos, |r| <= pi/4, < 1 ulp).
+// The angle never needs the large-argument (Payne-Hanek) path a general
+// libm sin/cos carries (scratch memory, registers).
+__device__ inline void mc_sincos(double x, double *sn, double *cs) {
+    const double q = rint(x * 0.63661977236758134308);  // 2/pi
+    double r = fma(-q, 1.57079632673412561417e+00, x);
+    r = fma(-q, 6.07710050630396597660e-11, r);
+    r = fma(-q, 2.02226624879595063154e-21, r);
+    const double z = r * r;
+    const double ps = fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
+                                         2.75573137070700676789e-06), -1.98412698298579493134e-04),
+                          8.33333333332248946124e-03);
+    const double sr = fma(r * z, fma(z, ps, -1.66666666666666324348e-01), r);
+    const double pc = z * fma(z, fma(z, fma(z, fma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+                                                 -2.75573143513906633035e-07), 2.48015872894767294178e-05),
+                                      -1.38888888888741095749e-03), 4.16666666666666019037e-02);
+    const double hz = 0.5 * z, w = 1.0 - hz;
+    const double cr = w + (((1.0 - w) - hz) + z * pc);
+    switch ((int)q & 3) {
+        case 0: *sn = sr; *cs = cr; break;
+        case 1: *sn = cr; *cs = -sr; break;
+        case 2: *sn = -sr; *cs = -cr; break;
+        default: *sn = -cr; *cs = sr; break;
+    }
+}
+
 __global__ __launch_bounds__(64) void mc_frames_kernel(McChannel C, int64_t frame0, int64_t B,
                                                        uint8_t *__restrict__ msg_out, int32_t *__restrict__ sym_out) {
-    extern __shared__ uint8_t ux[];
+#pragma clang fp contract(off)
+    extern __shared__ uint32_t lds_mc[];
     const int t = threadIdx.x;
-    const int N = C.N, K = C.K;
+    const int N = C.N, K = C.K, A = C.A, M = C.n_edges - 1;
+    const int nw = (N + 31) >> 5;        // u / x words
+    const int kw = (K + 31) >> 5;        // information-bit words (message + CRC)
+    double *edges = reinterpret_cast<double *>(lds_mc);
+    int32_t *lut = reinterpret_cast<int32_t *>(edges + kMcMaxEdges);
+    uint32_t *xw = reinterpret_cast<uint32_t *>(lut + kMcMaxEdges);
+    uint32_t *bw = xw + nw;               // message + CRC bits (kw + 2 words)
+    for (int i = t; i < C.n_edges; i += 64) edges[i] = C.edges[i];
+    for (int i = t; i < M; i += 64) lut[i] = C.lut[i];
+    const double lo_edge = C.edges[0], hi_edge = C.edges[M];
+    const double inv_w = hi_edge > lo_edge ? M / (hi_edge - lo_edge) : 0.0;
     for (int64_t f = blockIdx.x; f < B; f += gridDim.x) {
         const uint64_t gid = (uint64_t)(frame0 + f);
         const uint32_t glo = (uint32_t)gid, ghi = (uint32_t)(gid >> 32);
-        for (int e = t; e < N; e += 64) ux[e] = 0;
-        __syncthreads();
-        const int A = C.A;  // message bits (= K without CRC)
-        for (int w = t; w * 128 < A; w += 64) {
-            const Philox4 r = philox4x32_10(glo, ghi, (uint32_t)w, kTagMsg, C.seed_lo, C.seed_hi);
-            for (int b = 0; b < 128 && 128 * w + b < A; ++b) {
-                const uint8_t bit = (r.v[b >> 5] >> (b & 31)) & 1u;
-                const int j = 128 * w + b;
-                msg_out[f * A + j] = bit;
-                ux[C.info_pos[j]] = bit;
+        // message dword d = Philox(w = d / 4).v[d % 4]; bits >= A cleared
+        uint32_t crc_part = 0;
+        for (int d = t; d < kw + 2; d += 64) {  // + 2 zero words: funnel reads past the last
+            uint32_t m = 0;
+            if (32 * d < A) {
+                const Philox4 r = philox4x32_10(glo, ghi, (uint32_t)(d >> 2), kTagMsg, C.seed_lo, C.seed_hi);
+                m = r.v[d & 3];
+                if (A - 32 * d < 32) m &= (1u << (A - 32 * d)) - 1u;
+                // msg bytes 32d .. 32d+31 (A % 8 == 0: 8 B stores)
+                uint8_t *mo = msg_out + f * A + 32 * d;
+                const int nb = min(32, A - 32 * d);
+                if ((A & 7) == 0 && nb == 32) {
+                    uint32_t w4[8];
+                    for (int k = 0; k < 8; ++k) {
+                        const uint32_t nib = (m >> (4 * k)) & 0xFu;
+                        w4[k] = (nib & 1u) | ((nib & 2u) << 7) | ((nib & 4u) << 14) | ((nib & 8u) << 21);
+                    }
+                    uint2 *o2 = reinterpret_cast<uint2 *>(mo);
+                    for (int k = 0; k < 4; ++k) o2[k] = make_uint2(w4[2 * k], w4[2 * k + 1]);
+                } else {
+                    for (int b = 0; b < nb; ++b) mo[b] = (uint8_t)((m >> b) & 1u);
+                }
+                if (C.crc_n > 0)
+                    for (uint32_t mm = m; mm; mm &= mm - 1u) crc_part ^= C.crc_tab[32 * d + __builtin_ctz(mm)];
             }
+            bw[d] = m;
+        }
+        if (C.crc_n > 0) {  // CRC::encoding (utils.cpp:77-92): XOR of the set bits' contributions
+            for (int s = 32; s >= 1; s >>= 1) crc_part ^= (uint32_t)__shfl_xor((int)crc_part, s, 64);
+            __syncthreads();
+            if (t == 0)
+                for (int j = 0; j < K - A; ++j) {
+                    const uint32_t bit = (crc_part >> (C.crc_n - 1 - j)) & 1u;
+                    bw[(A + j) >> 5] |= bit << ((A + j) & 31);
+                }
         }
         __syncthreads();
-        if (C.crc_n > 0 && t == 0) {  // CRC::encoding (utils.cpp:77-92) as a register, one lane
-            const uint32_t top = 1u << (C.crc_n - 1), mask = (top << 1) - 1u;
-            uint32_t r = 0;
-            for (int j = 0; j < A; ++j) {
-                const uint32_t fb = (uint32_t)ux[C.info_pos[j]] ^ ((r & top) ? 1u : 0u);
-                r = ((r << 1) & mask) ^ (C.crc_q & (0u - fb));
+        // u word w = the info bits [pref_w, pref_w + popc(mask_w)) deposited at the mask's set bits;
+        // then the 5 in-word stages of x = u F^{(x)n} (bit i ^= bit i + m for i with bit m clear)
+        for (int w = t; w < nw; w += 64) {
+            uint32_t mask = C.info_mask[w];
+            const int s = C.info_pref[w];
+            const uint32_t lo = bw[s >> 5], hi = bw[(s >> 5) + 1];
+            uint32_t src = (s & 31) ? ((lo >> (s & 31)) | (hi << (32 - (s & 31)))) : lo;
+            uint32_t u = 0;
+            for (; mask; mask &= mask - 1u) {
+                u |= (src & 1u) << __builtin_ctz(mask);
+                src >>= 1;
             }
-            for (int j = 0; j < K - A; ++j) ux[C.info_pos[A + j]] = (uint8_t)((r >> (C.crc_n - 1 - j)) & 1u);
+            u ^= (u >> 1) & 0x55555555u;
+            u ^= (u >> 2) & 0x33333333u;
+            u ^= (u >> 4) & 0x0F0F0F0Fu;
+            u ^= (u >> 8) & 0x00FF00FFu;
+            u ^= (u >> 16) & 0x0000FFFFu;
+            xw[w] = u;
         }
         __syncthreads();
-        for (int m = 1; m < N; m *= 2) {  // x = u F^{(x)n}
-            for (int e = t; e < N / 2; e += 64) {
-                const int i = (e / m) * 2 * m + (e % m);
-                ux[i] ^= ux[i + m];
-            }
+        for (int sw = 1; sw < nw; sw <<= 1) {  // word stages (m = 32 sw)
+            for (int w = t; w < nw; w += 64)
+                if (!(w & sw)) xw[w] ^= xw[w + sw];
             __syncthreads();
         }
+        // AWGN + LLR + channel quantizer, positions 2p and 2p+1
         for (int p = t; 2 * p < N; p += 64) {
             const Philox4 r = philox4x32_10(glo, ghi, (uint32_t)p, kTagNoise, C.seed_lo, C.seed_hi);
-            const float u1 = ((float)(r.v[0] >> 8) + 0.5f) * (1.0f / 16777216.0f);
-            const float u2 = (float)(r.v[1] >> 8) * (1.0f / 16777216.0f);
-            const float rad = sqrtf(-2.0f * logf(u1));
-            float s, c;
-            sincosf(6.283185307179586f * u2, &s, &c);
-            const float nz[2] = {rad * c, rad * s};
+            const double u1 = (double)(mc_u53(r.v[0], r.v[1]) + 1u) * 0x1p-53;  // (0, 1]
+            const double u2 = (double)mc_u53(r.v[2], r.v[3]) * 0x1p-53;         // [0, 1)
+            const double rad = sqrt(-2.0 * log(u1));
+            double sn, cs;
+            mc_sincos(6.283185307179586 * u2, &sn, &cs);
+            const double nz[2] = {rad * cs, rad * sn};
+            const uint32_t xbits = xw[(2 * p) >> 5] >> ((2 * p) & 31);
+            int s_out[2];
             for (int h = 0; h < 2; ++h) {
-                const int e = 2 * p + h;
-                const float y = (1.0f - 2.0f * (float)ux[e]) + C.sigma * nz[h];
-                const double llr = (double)(y * C.llr_scale);
-                int s_out;
-                const int M = C.n_edges - 1;
-                if (llr <= C.edges[0]) {
-                    s_out = 0;
-                } else if (llr >= C.edges[M]) {
-                    s_out = C.q - 1;
-                } else {  // bisect_left over edges[0..M-1]
-                    int lo = 0, hi = M;
-                    while (lo < hi) {
-                        const int mid = (lo + hi) >> 1;
-                        if (C.edges[mid] < llr)
-                            lo = mid + 1;
-                        else
-                            hi = mid;
-                    }
-                    s_out = C.lut[lo - 1];
+                const double bpsk = (xbits >> h) & 1u ? -1.0 : 1.0;
+                const double y = bpsk + C.sigma * nz[h];
+                const double llr = y * 2.0 / C.s2;
+                if (llr <= lo_edge) {
+                    s_out[h] = 0;
+                } else if (llr >= hi_edge) {
+                    s_out[h] = C.q - 1;
+                } else {  // bisect_left over edges[0..M-1]: a guess from the mean bin width, then walk
+                    int lo = (int)((llr - lo_edge) * inv_w);
+                    lo = lo < 0 ? 0 : (lo > M ? M : lo);
+                    while (lo > 0 && edges[lo - 1] >= llr) --lo;
+                    while (lo < M && edges[lo] < llr) ++lo;
+                    s_out[h] = lut[lo - 1];
                 }
-                sym_out[f * N + e] = s_out;
             }
+            *reinterpret_cast<int2 *>(sym_out + f * N + 2 * p) = make_int2(s_out[0], s_out[1]);
         }
         __syncthreads();
     }
+}
+
+// Dynamic LDS of mc_frames_kernel.
+inline size_t mc_lds_bytes(int N, int K) {
+    return kMcMaxEdges * (sizeof(double) + sizeof(int32_t)) + 4 * (((N + 31) >> 5) + ((K + 31) >> 5) + 2);
 }
 
 }  // namespace qpd

@@ -1,6 +1,6 @@
 """Test-side restatement of the qpd_mc_frames generator (csrc/qpd_mc.hip):
 Philox4x32-10 keyed by (seed, global frame id), message bits, polar encoding,
-BPSK + AWGN (float32 Box-Muller), LLR and the driver's channel quantizer."""
+BPSK + AWGN (float64 Box-Muller on 53-bit uniforms), LLR and the driver's channel quantizer."""
 import numpy as np
 
 from quantized_decoder_polar_codes_amd import codes as C
@@ -25,6 +25,11 @@ def philox(c0, c1, c2, c3, k0, k1):
     return c0, c1, c2, c3
 
 
+def u53(a, b):
+    """53-bit uniform integer from two Philox words (qpd_mc.hip mc_u53)."""
+    return ((a >> np.uint64(5)) << np.uint64(26)) | (b >> np.uint64(6))
+
+
 def frames(N, K, msgbits, seed, frame0, B, sigma, edges, lut, q, A=None, crc=None):
     """crc = (crc_n, loc): the message is A bits followed by the first K-A bits of
     their CRC (oracle.crc_encode, the reference's CRC::encoding); returns the A bits."""
@@ -47,16 +52,17 @@ def frames(N, K, msgbits, seed, frame0, B, sigma, edges, lut, q, A=None, crc=Non
         u = np.concatenate([msg, oracle.crc_encode(msg, crc[0], crc[1])[:, : K - A]], axis=1)
     x = C.polar_encode(u, msgbits, N)
     llr = np.zeros((B, N), dtype=np.float64)
+    s2 = np.float64(sigma) * np.float64(sigma)  # the driver's sigma ** 2
     for p in range(N // 2):
         r = philox(glo, ghi, np.full(B, p, np.uint64), np.full(B, TAG_NOISE, np.uint64), slo, shi)
-        u1 = ((r[0] >> np.uint64(8)).astype(np.float32) + np.float32(0.5)) * np.float32(1.0 / 16777216.0)
-        u2 = (r[1] >> np.uint64(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
-        rad = np.sqrt(np.float32(-2.0) * np.log(u1))
-        ang = np.float32(6.283185307179586) * u2
+        u1 = (u53(r[0], r[1]) + np.uint64(1)).astype(np.float64) * 2.0 ** -53  # (0, 1]
+        u2 = u53(r[2], r[3]).astype(np.float64) * 2.0 ** -53  # [0, 1)
+        rad = np.sqrt(-2.0 * np.log(u1))
+        ang = 6.283185307179586 * u2
         nz = (rad * np.cos(ang), rad * np.sin(ang))
         for h in range(2):
             e = 2 * p + h
-            y = (np.float32(1.0) - np.float32(2.0) * x[:, e].astype(np.float32)) + np.float32(sigma) * nz[h]
-            llr[:, e] = (y * np.float32(2.0 / (sigma * sigma))).astype(np.float64)
+            y = (1.0 - 2.0 * x[:, e].astype(np.float64)) + np.float64(sigma) * nz[h]  # y = bpsk + normal(0, sigma)
+            llr[:, e] = y * 2.0 / s2  # mainQuantizedDecoder_LLRDomain.py:165
     sym = C.quantize_channel(llr, edges, lut, q)
     return msg, sym, llr
