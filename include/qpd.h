@@ -111,7 +111,7 @@ typedef struct qpd_config {
     int32_t kind;               /* enum qpd_kind                                  */
     int32_t N;                  /* code length, power of two, 2..65536            */
     int32_t K;                  /* output bits = number of 0 entries in frozen    */
-    int32_t L;                  /* list size (SCL kinds), 1..8; ignored otherwise */
+    int32_t L;                  /* list size (SCL kinds), 1..32 (> 8: generic engine); ignored otherwise */
     int32_t v;                  /* symbol alphabet size, 2..256 (LUT kinds); the
                                    re-quantizer's v (uniform kinds: M = (v/2 - 0.5) r_f,
                                    (v/2 - 1) r_g, integer v/2)                    */

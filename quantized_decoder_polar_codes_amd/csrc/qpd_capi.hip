@@ -232,8 +232,8 @@ int validate(const qpd_config *c, int *n_out, int *fam_out, int *dom_out) {
     *fam_out = fam;
     *dom_out = dom;
     const bool list = fam == QPD_SCL_LUT || fam == QPD_FASTSCL_LUT;
-    if (list && (c->L < 1 || c->L > qpd::kMaxL))
-        return fail(QPD_E_UNSUPPORTED, "list size L must be in [1, 8] (2L <= 16: libstdc++ insertion-sort regime)");
+    if (list && (c->L < 1 || c->L > qpd::kMaxLWide))
+        return fail(QPD_E_UNSUPPORTED, "list size L must be in [1, 32]");
     if (fam == QPD_FASTSC_LUT || fam == QPD_FASTSCL_LUT) {
         if (!c->node_type) return fail(QPD_E_INVALID, "node_type is required for the Fast decoders");
         if (special_of(fam, c->node_type, 0) >= 0)
@@ -692,35 +692,44 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
 // Generic-engine instantiations generic_decode_kernel<family, domain>: every
 // family in the LUT and plain float domains; the re-quantized domains exist
 // only for SC and SCL (SC{,L}{Uniform,Lloyd}QuantizedDecoder).
-const void *generic_kernel(int fam, int dom) {
+const void *generic_kernel(int fam, int dom, bool wide) {
     using namespace qpd;
-#define QPD_GK(K, D) reinterpret_cast<const void *>(&generic_decode_kernel<K, D>)
-#define QPD_GK4(D)                                             \
-    switch (fam) {                                             \
-        case QPD_SC_LUT: return QPD_GK(K_SC_LUT, D);           \
-        case QPD_SCL_LUT: return QPD_GK(K_SCL_LUT, D);         \
-        case QPD_FASTSC_LUT: return QPD_GK(K_FASTSC_LUT, D);   \
-        case QPD_FASTSCL_LUT: return QPD_GK(K_FASTSCL_LUT, D); \
-        default: return nullptr;                               \
-    }
+#define QPD_GK(K, D) (wide ? reinterpret_cast<const void *>(&generic_decode_kernel<K, D, kMaxLWide>) \
+                           : reinterpret_cast<const void *>(&generic_decode_kernel<K, D, kMaxL>))
+#define QPD_GN(K, D) reinterpret_cast<const void *>(&generic_decode_kernel<K, D, kMaxL>)
+    // single-path families never need the wide list instantiation
     switch (dom) {
-        case DOM_LUT: QPD_GK4(DOM_LUT)
-        case DOM_FLOAT: QPD_GK4(DOM_FLOAT)
+        case DOM_LUT:
+            switch (fam) {
+                case QPD_SC_LUT: return QPD_GN(K_SC_LUT, DOM_LUT);
+                case QPD_SCL_LUT: return QPD_GK(K_SCL_LUT, DOM_LUT);
+                case QPD_FASTSC_LUT: return QPD_GN(K_FASTSC_LUT, DOM_LUT);
+                case QPD_FASTSCL_LUT: return QPD_GK(K_FASTSCL_LUT, DOM_LUT);
+                default: return nullptr;
+            }
+        case DOM_FLOAT:
+            switch (fam) {
+                case QPD_SC_LUT: return QPD_GN(K_SC_LUT, DOM_FLOAT);
+                case QPD_SCL_LUT: return QPD_GK(K_SCL_LUT, DOM_FLOAT);
+                case QPD_FASTSC_LUT: return QPD_GN(K_FASTSC_LUT, DOM_FLOAT);
+                case QPD_FASTSCL_LUT: return QPD_GK(K_FASTSCL_LUT, DOM_FLOAT);
+                default: return nullptr;
+            }
         case DOM_UNIFORM:
-            return fam == QPD_SC_LUT ? QPD_GK(K_SC_LUT, DOM_UNIFORM)
+            return fam == QPD_SC_LUT ? QPD_GN(K_SC_LUT, DOM_UNIFORM)
                                      : fam == QPD_SCL_LUT ? QPD_GK(K_SCL_LUT, DOM_UNIFORM) : nullptr;
         case DOM_LLOYD:
-            return fam == QPD_SC_LUT ? QPD_GK(K_SC_LUT, DOM_LLOYD)
+            return fam == QPD_SC_LUT ? QPD_GN(K_SC_LUT, DOM_LLOYD)
                                      : fam == QPD_SCL_LUT ? QPD_GK(K_SCL_LUT, DOM_LLOYD) : nullptr;
         default: return nullptr;
     }
-#undef QPD_GK4
+#undef QPD_GN
 #undef QPD_GK
 }
 
 template <class In>
 int launch_generic(qpd_decoder *d, const In *in, int64_t B, uint8_t *out, int grid, hipStream_t st) {
-    const void *kfn = generic_kernel(d->kind, d->dom);
+    const void *kfn = generic_kernel(d->kind, d->dom, d->L > qpd::kMaxL);
     if (!kfn) return fail(QPD_E_INVALID, "bad kind");
     qpd::DevPlan P = d->plan;
     const In *in_arg = in;
@@ -779,13 +788,14 @@ int qpd_create(const qpd_config *cfg, qpd_decoder **out) {
     visit(s, c->kind, c->N, n, c->frozen_bits, (c->kind == QPD_FASTSC_LUT || c->kind == QPD_FASTSCL_LUT) ? c->node_type : nullptr, 0, 0);
     d->ops_host = s.ops;
     {
-        const bool fast_ok = dom == qpd::DOM_LUT && c->f_step == 0 && c->g_step == 0 && c->v <= 16;
+        // L > 8 (2L > 16: libstdc++ introsort replayed per selection) runs on the generic engine
+        const bool fast_ok = dom == qpd::DOM_LUT && c->f_step == 0 && c->g_step == 0 && c->v <= 16 && d->L <= qpd::kMaxL;
         int want = c->engine;
         if (const char *e = getenv("QPD_ENGINE")) want = atoi(e);
         if (want == QPD_ENGINE_FAST && !fast_ok) {
             delete d;
             return fail(QPD_E_UNSUPPORTED,
-                        "fast engine needs LUT symbols with one table per node (f_step = g_step = 0) and v <= 16");
+                        "fast engine needs LUT symbols with one table per node (f_step = g_step = 0), v <= 16 and L <= 8");
         }
         d->engine = (want == QPD_ENGINE_GENERIC || !fast_ok) ? QPD_ENGINE_GENERIC : QPD_ENGINE_FAST;
     }

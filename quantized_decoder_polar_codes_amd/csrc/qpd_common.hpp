@@ -24,8 +24,9 @@ struct Op {
 };
 
 constexpr int kMaxDepth = 16;  // N <= 65536
-constexpr int kMaxL = 8;       // 2L <= 16: libstdc++ sorts by insertion (stable)
+constexpr int kMaxL = 8;       // fast engine: 2L <= 16, libstdc++ sorts by insertion (stable)
 constexpr int kMaxM = kMaxL - 1;
+constexpr int kMaxLWide = 32;  // generic engine: 2L <= 64, libstdc++ introsort replayed (stl_sort.hpp)
 
 // Decoder families of the kernels (the float-domain decoders use the same
 // family ids with a DOM_* symbol domain; K_SC_FLOAT is the C-ABI's kind 0).
@@ -196,15 +197,22 @@ __device__ __forceinline__ Sel select_survivors8(double kk, double kf, int gl, i
 // leading coefficient only clears the current bit, `crc_q` holds
 // coefficients 1..crc_n.  `word(w)` = this lane's decoded bits 32w..32w+31;
 // `info_mask` = wave-uniform information-position mask words.
-template <class WordFn>
-__device__ __forceinline__ int ca_winner(double pm, int gl, int gbase, int L, int N, const uint32_t *info_mask, int A,
-                                         int chk, int crc_n, uint32_t crc_q, WordFn word) {
-    const int K = A + chk;
+// Stable rank of this lane's path metric among the group's L (argsort by
+// insertion sort: L <= 16).
+__device__ __forceinline__ int stable_rank(double pm, int gl, int gbase, int L) {
     int rank = 0;
     for (int j = 0; j < L; ++j) {
         const double o = shfld(pm, gbase + j);
         rank += (o < pm) || (o == pm && j < gl);
     }
+    return rank;
+}
+
+// `rank` = this path's position in the argsort(PML) order.
+template <class WordFn>
+__device__ __forceinline__ int ca_winner_ranked(int rank, int gl, int gbase, int L, int N, const uint32_t *info_mask,
+                                                int A, int chk, int crc_n, uint32_t crc_q, WordFn word) {
+    const int K = A + chk;
     const uint32_t top = 1u << (crc_n - 1);
     const uint32_t mask = (top << 1) - 1u;  // crc_n = 32: 0 - 1 = all ones
     uint32_t r = 0;
@@ -228,7 +236,7 @@ __device__ __forceinline__ int ca_winner(double pm, int gl, int gbase, int L, in
             ++t;
         }
     }
-    const int key = gl < L ? (pass ? rank : 8 + rank) : 64;
+    const int key = gl < L ? (pass ? rank : kMaxLWide + rank) : 2 * kMaxLWide;
     int best = 0, bk = 1 << 30;
     for (int j = 0; j < L; ++j) {
         const int kj = __shfl(key, gbase + j);
@@ -238,6 +246,12 @@ __device__ __forceinline__ int ca_winner(double pm, int gl, int gbase, int L, in
         }
     }
     return best;
+}
+
+template <class WordFn>
+__device__ __forceinline__ int ca_winner(double pm, int gl, int gbase, int L, int N, const uint32_t *info_mask, int A,
+                                         int chk, int crc_n, uint32_t crc_q, WordFn word) {
+    return ca_winner_ranked(stable_rank(pm, gl, gbase, L), gl, gbase, L, N, info_mask, A, chk, crc_n, crc_q, word);
 }
 
 }  // namespace qpd

@@ -205,6 +205,121 @@ struct LaneSortSeq {
     __device__ bool less(int a, int b) { return key(a) < key(b); }
 };
 
+// List pointer words (pointer memory): per tree depth, the lane-in-group whose
+// slot holds the path's data.  4-bit fields in 64 bits for lane groups of up
+// to 16 lanes (L <= 8 instantiations), 5-bit fields in 128 bits for groups of
+// 32 (the wide instantiations, L <= 32).
+template <int ML>
+struct PtrW {
+    using T = uint64_t;
+    static constexpr int B = 4;
+};
+template <>
+struct PtrW<kMaxLWide> {
+    using T = unsigned __int128;
+    static constexpr int B = 5;
+};
+
+template <int ML>
+__device__ __forceinline__ int gp_get(typename PtrW<ML>::T p, int d) {
+    return (int)(p >> (PtrW<ML>::B * d)) & ((1 << PtrW<ML>::B) - 1);
+}
+
+template <int ML>
+__device__ __forceinline__ typename PtrW<ML>::T gp_set(typename PtrW<ML>::T p, int d, int v) {
+    using T = typename PtrW<ML>::T;
+    const T m = (T)((1u << PtrW<ML>::B) - 1u) << (PtrW<ML>::B * d);
+    return (p & ~m) | ((T)(unsigned)v << (PtrW<ML>::B * d));
+}
+
+template <int ML>
+__device__ __forceinline__ typename PtrW<ML>::T gp_shfl(typename PtrW<ML>::T x, int src) {
+    if constexpr (ML == kMaxLWide) {
+        const uint64_t lo = shfl64((uint64_t)x, src), hi = shfl64((uint64_t)(x >> 64), src);
+        return ((unsigned __int128)hi << 64) | lo;
+    } else {
+        return shfl64(x, src);
+    }
+}
+
+// Index arrays sorted in LDS by their keys (stl_sort.hpp Seq interface).
+struct LdsSortSeq {
+    int *idx;
+    const double *key;
+    __device__ int get(int p) { return idx[p]; }
+    __device__ void set(int p, int e) { idx[p] = e; }
+    __device__ bool less(int a, int b) { return key[a] < key[b]; }
+};
+
+// LDS of the list selection: ranks (sel) and, for 2L > 16, the candidate
+// keys and index array the group's lane 0 sorts.
+struct ListLds {
+    int sel[64];
+    int idx[128];
+    double key[128];
+};
+
+// Survivor selection, mink (src/SCLLUTDecoder.cpp:8-21): 2L <= 16 by stable
+// ranks (insertion sort); 2L > 16 (wide instantiations) by replaying
+// libstdc++'s introsort of the 2L candidates [PML_0..L-1, PML_i + |DM_i|] on
+// lane 0 of each group and taking the first L (H1).
+template <int ML>
+__device__ __forceinline__ Sel gselect(double kk, double kf, int gl, int gbase, int L, ListLds &sh) {
+    if constexpr (ML == kMaxLWide) {
+        if (2 * L > stl::kThreshold) {
+            double *key = sh.key + 2 * gbase;
+            int *idx = sh.idx + 2 * gbase;
+            if (gl < L) {
+                key[gl] = kk;
+                key[L + gl] = kf;
+            }
+            lds_order();
+            if (gl == 0) {
+                LdsSortSeq seq{idx, key};
+                for (int p = 0; p < 2 * L; ++p) idx[p] = p;
+                if (2 * L <= 2 * stl::kThreshold + 1)
+                    stl::sort_small_prefix(seq, 0, 2 * L, L);
+                else
+                    stl::sort(seq, 0, 2 * L);
+                for (int i = 0; i < L; ++i) sh.sel[gbase + i] = idx[i];
+            }
+            lds_order();
+            const int c = gl < L ? sh.sel[gbase + gl] : gl;
+            lds_order();
+            Sel s;
+            s.upper = c >= L;
+            s.parent = s.upper ? c - L : c;
+            return s;
+        }
+    }
+    return select_survivors(kk, kf, gl, gbase, L, sh.sel);
+}
+
+// Position of this path in argsort(PML) (the CA epilogue, CASCLLUTDecoder.cpp:264):
+// stable for L <= 16, the introsort replay above that.
+template <int ML>
+__device__ __forceinline__ int grank(double pm, int gl, int gbase, int L, ListLds &sh) {
+    if constexpr (ML == kMaxLWide) {
+        if (L > stl::kThreshold) {
+            double *key = sh.key + 2 * gbase;
+            int *idx = sh.idx + 2 * gbase;
+            if (gl < L) key[gl] = pm;
+            lds_order();
+            if (gl == 0) {
+                LdsSortSeq seq{idx, key};
+                for (int p = 0; p < L; ++p) idx[p] = p;
+                stl::sort_small(seq, 0, L);
+                for (int i = 0; i < L; ++i) sh.sel[gbase + idx[i]] = i;
+            }
+            lds_order();
+            const int r = gl < L ? sh.sel[gbase + gl] : 0;
+            lds_order();
+            return r;
+        }
+    }
+    return stable_rank(pm, gl, gbase, L);
+}
+
 // A NaN path metric would reach std::sort (UB in the reference): flag it.
 template <int DOM>
 __device__ __forceinline__ void check_keys(const DevPlan &P, double a, double b) {
@@ -216,7 +331,7 @@ __device__ __forceinline__ void check_keys(const DevPlan &P, double a, double b)
 // ---------------------------------------------------------------------------
 // The decoders.  KIND = family (SC / SCL / FastSC / FastSCL), DOM = domain.
 // ---------------------------------------------------------------------------
-template <int KIND, int DOM>
+template <int KIND, int DOM, int ML>
 __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
                                                             const std::conditional_t<DOM == DOM_LUT, int32_t, double>
                                                                 *__restrict__ in,
@@ -224,7 +339,9 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
     constexpr bool kList = (KIND == K_SCL_LUT || KIND == K_FASTSCL_LUT);
     constexpr bool kLut = DOM == DOM_LUT;
     using In = std::conditional_t<kLut, int32_t, double>;
-    __shared__ int sel[64];
+    __shared__ ListLds sh;
+    using PT = typename PtrW<ML>::T;
+    constexpr int MM = ML - 1;  // R1 layers kept in registers: min(L - 1, temp)
     const int lane = threadIdx.x;
     const int gs = P.gs;
     const int gl = lane & (gs - 1);
@@ -235,8 +352,8 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
     uint32_t *wsc = P.scratch + (size_t)blockIdx.x * P.rows_per_wave * 64;
     const int64_t ngroups = (B + P.fpw - 1) / P.fpw;
 
-    uint64_t self = 0;
-    for (int d = 0; d < kMaxDepth; ++d) self |= (uint64_t)gl << (4 * d);
+    PT self = 0;
+    for (int d = 0; d <= kMaxDepth && PtrW<ML>::B * (d + 1) <= (int)(8 * sizeof(PT)); ++d) self = gp_set<ML>(self, d, gl);
 
     for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
         int64_t frame = grp * P.fpw + lane / gs;
@@ -244,7 +361,7 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
         if (!frame_ok) frame = B - 1;
         const In *y = in + frame * (int64_t)N;
         double pm = (gl == 0) ? 0.0 : P.pm_init;
-        uint64_t ps = self, pu = self;
+        PT ps = self, pu = self;
 
         for (int oi = 0; oi < P.nops; ++oi) {
             const Op op = P.ops[oi];
@@ -255,8 +372,8 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
                 case OP_G: {
                     const bool isg = op.type == OP_G;
                     const int ctemp = N >> (d + 1);
-                    const int src = gbase + ptr_get(ps, d);
-                    const int usrc = gbase + ptr_get(pu, d + 1);
+                    const int src = gbase + gp_get<ML>(ps, d);
+                    const int usrc = gbase + gp_get<ML>(pu, d + 1);
                     if constexpr (kLut) {
                         const uint8_t *T = isg ? P.lut_g : P.lut_f;
                         const int tsz = isg ? 2 * vv : vv;
@@ -293,7 +410,7 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
                             set_fval(P, wsc, d + 1, e, lane, r);
                         }
                     }
-                    ps = ptr_set(ps, d + 1, gl);
+                    ps = gp_set<ML>(ps, d + 1, gl);
                     break;
                 }
                 case OP_LEAF_L:
@@ -301,7 +418,7 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
                     const bool right = op.type == OP_LEAF_R;
                     const int k = 2 * node + (right ? 1 : 0);
                     const bool frozen = op.aux != 0;
-                    const int src = gbase + ptr_get(ps, d);
+                    const int src = gbase + gp_get<ML>(ps, d);
                     uint32_t dec = 0;
                     if (!kList && frozen) {
                         dec = 0;  // SCLUTDecoder.cpp:60-61 / SCDecoder.cpp:25-26: frozen leaves are 0
@@ -312,7 +429,7 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
                         if constexpr (kLut) {
                             int s;
                             if (right) {
-                                const int u = row_ptr(wsc, P.Uo[n])[gbase + ptr_get(pu, n)] & 1;
+                                const int u = row_ptr(wsc, P.Uo[n])[gbase + gp_get<ML>(pu, n)] & 1;
                                 s = P.lut_g[(size_t)P.g_base[posi] * 2 * vv + u * vv + a * v + b];
                             } else {
                                 s = P.lut_f[(size_t)P.f_base[posi] * vv + a * v + b];
@@ -320,7 +437,7 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
                             dm = vcl_at(P, n - 1, k, s);  // H3: row n-1
                         } else {
                             if (right) {
-                                const int u = row_ptr(wsc, P.Uo[n])[gbase + ptr_get(pu, n)] & 1;
+                                const int u = row_ptr(wsc, P.Uo[n])[gbase + gp_get<ML>(pu, n)] & 1;
                                 dm = fd_g<DOM>(P, posi, u, a, b);
                             } else {
                                 dm = fd_f<DOM>(P, posi, a, b);
@@ -334,26 +451,26 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
                         } else {
                             const double kf = pm + fabs(dm);
                             check_keys<DOM>(P, pm, kf);
-                            const Sel sl = select_survivors(pm, kf, gl, gbase, L, sel);
+                            const Sel sl = gselect<ML>(pm, kf, gl, gbase, L, sh);
                             const int p = gbase + sl.parent;
                             const uint32_t hd = dm < 0;  // H4: SCL family `< 0`
                             dec = (uint32_t)__shfl((int)hd, p) ^ (sl.upper ? 1u : 0u);
                             pm = pick(sl.upper, shfld(kf, p), shfld(pm, p));
-                            ps = shfl64(ps, p);
-                            pu = shfl64(pu, p);
+                            ps = gp_shfl<ML>(ps, p);
+                            pu = gp_shfl<ML>(pu, p);
                         }
                     }
                     if (right) {
                         row_ptr(wsc, P.Ro)[lane] = dec;
                     } else {
                         row_ptr(wsc, P.Uo[n])[lane] = dec;
-                        pu = ptr_set(pu, n, gl);
+                        pu = gp_set<ML>(pu, n, gl);
                     }
                     break;
                 }
                 case OP_COMB: {
                     const int ctemp = N >> (d + 1);
-                    const int usrc = gbase + ptr_get(pu, d + 1);
+                    const int usrc = gbase + gp_get<ML>(pu, d + 1);
                     const bool to_r = (d == 0) || (node & 1);
                     if (ctemp < 32) {
                         const uint32_t m = (1u << ctemp) - 1u;
@@ -369,13 +486,13 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
                             store_node_word(P, wsc, d, to_r, w, ul ^ r, lane);
                         }
                     }
-                    if (!to_r) pu = ptr_set(pu, d, gl);
+                    if (!to_r) pu = gp_set<ML>(pu, d, gl);
                     break;
                 }
                 default: {  // special nodes, FastSCLUT.cpp:46-107 / FastSCLLUTDecoder.cpp:82-213,
                             // FastSCDecoder.cpp:45-106 / FastSCLDecoder.cpp:122-251
                     const int temp = N >> d;
-                    const int src = gbase + ptr_get(ps, d);
+                    const int src = gbase + gp_get<ML>(ps, d);
                     const bool to_r = (node & 1);
                     const int base_pos = temp * node;
                     const int nwo = (temp + 31) >> 5;
@@ -407,11 +524,11 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
                                 kf += (double)(l >= 0) * fabs(l);
                             }
                             check_keys<DOM>(P, kk, kf);
-                            const Sel sl = select_survivors(kk, kf, gl, gbase, L, sel);
+                            const Sel sl = gselect<ML>(kk, kf, gl, gbase, L, sh);
                             const int p = gbase + sl.parent;
                             pm = pick(sl.upper, shfld(kf, p), shfld(kk, p));
-                            ps = shfl64(ps, p);
-                            pu = shfl64(pu, p);
+                            ps = gp_shfl<ML>(ps, p);
+                            pu = gp_shfl<ML>(pu, p);
                             fill = sl.upper ? 0xffffffffu : 0u;
                         }
                         const uint32_t m = temp < 32 ? ((1u << temp) - 1u) : 0xffffffffu;
@@ -464,11 +581,11 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
                             row_ptr(wsc, P.Ho + w)[lane] = word;
                         }
                         // first m entries of argsort(|l|) (argsort :7-17, H1)
-                        int ord[kMaxM];
-                        double ms[kMaxM];
-                        int flip[kMaxM];
+                        int ord[MM];
+                        double ms[MM];
+                        int flip[MM];
 #pragma unroll
-                        for (int q = 0; q < kMaxM; ++q) {
+                        for (int q = 0; q < MM; ++q) {
                             ord[q] = 0;
                             ms[q] = 0;
                             flip[q] = -1;
@@ -478,7 +595,7 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
                             // insertion sort is stable: order by (|l|, index)
                             uint32_t taken = 0;
 #pragma unroll
-                            for (int q = 0; q < kMaxM; ++q) {
+                            for (int q = 0; q < MM; ++q) {
                                 if (q < m) {
                                     int bj = -1;
                                     double bk = 0;
@@ -499,7 +616,7 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
                             for (int p = 0; p < temp; ++p) seq.set(p, p);
                             stl::sort(seq, 0, temp);
 #pragma unroll
-                            for (int q = 0; q < kMaxM; ++q) {
+                            for (int q = 0; q < MM; ++q) {
                                 if (q < m) {
                                     ord[q] = seq.get(q);
                                     ms[q] = seq.key(ord[q]);
@@ -509,19 +626,19 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
                         wave_sync();  // H rows visible to the other lanes of the group
                         int origin = gl;
 #pragma unroll
-                        for (int layer = 0; layer < kMaxM; ++layer) {
+                        for (int layer = 0; layer < MM; ++layer) {
                             if (layer < m) {
                                 const double kf = pm + ms[layer];
                                 check_keys<DOM>(P, pm, kf);
-                                const Sel sl = select_survivors(pm, kf, gl, gbase, L, sel);
+                                const Sel sl = gselect<ML>(pm, kf, gl, gbase, L, sh);
                                 const int p = gbase + sl.parent;
                                 const int pos_old = ord[layer];  // H2: own pre-permutation order
                                 pm = pick(sl.upper, shfld(kf, p), shfld(pm, p));
-                                ps = shfl64(ps, p);
-                                pu = shfl64(pu, p);
+                                ps = gp_shfl<ML>(ps, p);
+                                pu = gp_shfl<ML>(pu, p);
                                 origin = __shfl(origin, p);
 #pragma unroll
-                                for (int q = 0; q < kMaxM; ++q) {
+                                for (int q = 0; q < MM; ++q) {
                                     ord[q] = __shfl(ord[q], p);
                                     ms[q] = shfld(ms[q], p);
                                     if (q < layer) flip[q] = __shfl(flip[q], p);
@@ -532,13 +649,13 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
                         for (int w = 0; w < nwo; ++w) {
                             uint32_t word = row_ptr(wsc, P.Ho + w)[gbase + origin];
 #pragma unroll
-                            for (int q = 0; q < kMaxM; ++q)
+                            for (int q = 0; q < MM; ++q)
                                 if (q < m && flip[q] >= 0 && (flip[q] >> 5) == w) word ^= 1u << (flip[q] & 31);
                             if (temp < 32) word &= (1u << temp) - 1u;
                             store_node_word(P, wsc, d, to_r, w, word, lane);
                         }
                     }
-                    if (!to_r) pu = ptr_set(pu, d, gl);
+                    if (!to_r) pu = gp_set<ML>(pu, d, gl);
                     break;
                 }
             }
@@ -570,8 +687,8 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
         int best = 0;
         if (kList && P.crc_n > 0) {
             check_keys<DOM>(P, pm, pm);  // the CA epilogue sorts the metrics
-            best = ca_winner(pm, gl, gbase, L, P.N, P.info_mask, P.ca_A, P.ca_chk, P.crc_n, P.crc_q,
-                             [&](int w) { return row_ptr(wsc, P.Ro + w)[lane]; });
+            best = ca_winner_ranked(grank<ML>(pm, gl, gbase, L, sh), gl, gbase, L, P.N, P.info_mask, P.ca_A, P.ca_chk,
+                                    P.crc_n, P.crc_q, [&](int w) { return row_ptr(wsc, P.Ro + w)[lane]; });
         } else if (kList) {
             double bpm = shfld(pm, gbase);
             for (int j = 1; j < L; ++j) {

@@ -200,6 +200,25 @@ def main_ca():
     make_ca_case(R, "ca_fastscllut_n1024_a488_l8_minsum", "CA-FastSCL-LUT", 1024, 488, 8, "minsum", 150, 1.5, 15)
 
 
+def main_wide():
+    """List sizes above 8: 2L > 16 puts the reference's mink (and, for L > 16,
+    the CA epilogue's argsort) into libstdc++'s introsort (H1); tie-heavy
+    tables make the tie order visible."""
+    R = O.reference_module()
+    if R is None:
+        raise SystemExit("oracle/_ref not built (run oracle/build_ref.sh)")
+    make_lut_case(R, "scllut_n128_k64_l16_random", "SCL-LUT", 128, 64, 16, "random", 300, 2.0, 31)
+    make_lut_case(R, "scllut_n128_k64_l32_random", "SCL-LUT", 128, 64, 32, "random", 150, 2.0, 32)
+    make_lut_case(R, "scllut_n128_k64_l12_random", "SCL-LUT", 128, 64, 12, "random", 200, 2.0, 33)
+    make_lut_case(R, "fastscllut_n128_k64_l16_random", "FastSCL-LUT", 128, 64, 16, "random", 300, 2.0, 34)
+    make_lut_case(R, "fastscllut_n128_k64_l32_random", "FastSCL-LUT", 128, 64, 32, "random", 150, 2.0, 35)
+    make_lut_case(R, "scllut_n1024_k512_l16_random", "SCL-LUT", 1024, 512, 16, "random", 60, 2.0, 36)
+    make_lut_case(R, "fastscllut_n1024_k512_l16_random", "FastSCL-LUT", 1024, 512, 16, "random", 60, 2.0, 37)
+    make_ca_case(R, "ca_scllut_n128_a40_l16_random", "CA-SCL-LUT", 128, 40, 16, "random", 200, 1.5, 38)
+    make_ca_case(R, "ca_scllut_n128_a40_l32_minsum", "CA-SCL-LUT", 128, 40, 32, "minsum", 150, 1.5, 39)
+    make_ca_case(R, "ca_fastscllut_n128_a40_l32_random", "CA-FastSCL-LUT", 128, 40, 32, "random", 150, 1.5, 40)
+
+
 def main_md():
     R = O.reference_module()
     if R is None:
@@ -214,7 +233,10 @@ if __name__ == "__main__":
         main_ca()  # only the CRC-aided fixtures
     elif sys.argv[1:] == ["md"]:
         main_md()  # only the MinDistortion (BASELINE workload) fixtures
+    elif sys.argv[1:] == ["wide"]:
+        main_wide()  # only the L > 8 fixtures
     else:
         main()
         main_ca()
         main_md()
+        main_wide()

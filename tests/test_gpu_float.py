@@ -57,7 +57,8 @@ def test_gpu_float_matches_golden(path, qpd):
 
 
 CASES = [(2, 1, 2), (4, 2, 2), (8, 4, 3), (16, 8, 4), (32, 16, 8), (64, 20, 5), (128, 64, 8), (256, 128, 7),
-         (512, 256, 8), (1024, 512, 8), (1024, 512, 1)]
+         (512, 256, 8), (1024, 512, 8), (1024, 512, 1),
+         (64, 40, 16), (128, 64, 32), (128, 70, 13)]  # L > 8: introsort replay of 2L > 16 candidates
 
 
 @pytest.mark.parametrize("style", ["awgn", "ties"])

@@ -56,7 +56,7 @@ def test_gpu_matches_golden(path, engine, qpd):
         kw = {"A": int(g["A"])} if str(g["kind"]).startswith("CA-") else {}
         dec = qpd.from_packed(str(g["kind"]), golden_packed(g), K, g["frozen"], L=L, node_type=g["node_type"],
                               engine=engine, **kw)
-        assert dec.info()["engine"] == (2 if engine == "auto" else 1)
+        assert dec.info()["engine"] == (2 if engine == "auto" and L <= 8 else 1)  # L > 8: generic engine
         got = dec.decode_batch(g["symbols"].astype(np.int32))
     bad = np.flatnonzero((got != g["expected"]).any(1))
     assert bad.size == 0, f"{bad.size}/{len(got)} frames differ, first {bad[:5]}"
@@ -76,6 +76,13 @@ CASES = [
     (512, 256, 8, "minsum"),
     (1024, 512, 8, "random"),
     (1024, 512, 1, "random"),
+    # L > 8: 2L > 16 candidates, libstdc++ introsort replayed per selection
+    (32, 16, 9, "random"),
+    (64, 32, 16, "random"),
+    (128, 64, 16, "minsum"),
+    (128, 80, 21, "random"),
+    (256, 128, 32, "random"),
+    (512, 256, 16, "perelem"),
 ]
 
 
@@ -105,7 +112,7 @@ def test_gpu_matches_oracle(N, K, L, tables, kind, engine, qpd, oracle_mod):
     want = oracle_mod.decode_lut(kind, p, K, L, fm, sym, node_type=nt)
     dec = qpd.from_packed(kind, p, K, fm, L=L, node_type=nt, engine=engine)
     if engine == "auto":
-        assert dec.info()["engine"] == (1 if tables == "perelem" else 2)
+        assert dec.info()["engine"] == (1 if tables == "perelem" or (L > 8 and kind in ("SCL-LUT", "FastSCL-LUT")) else 2)
     got = dec.decode_batch(sym)
     bad = np.flatnonzero((got != want).any(1))
     assert bad.size == 0, f"{bad.size}/{B} frames differ, first {bad[:5]}"
