@@ -150,7 +150,7 @@ def _cfg(kind=2, N=8, K=4, L=4, frozen=None, over=None):
 
 
 @pytest.mark.parametrize("over,code", [
-    ({"L": 9}, -2),            # 2L > 16 not supported
+    ({"L": 33}, -2),           # L > 32 not supported
     ({"L": 0}, -2),
     ({"N": 12}, -1),           # not a power of two
     ({"K": 3}, -1),            # K != number of information bits
