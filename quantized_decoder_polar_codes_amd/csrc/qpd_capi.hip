@@ -352,6 +352,12 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
         MOp m = base(OP_R0 + t);
         m.cnt = N >> d;
         m.vrow = (d - 1) * N + (N >> d) * node;
+        if (v <= 16 && !getenv("QPD_NO_VUNI")) {  // one quanta row for all the node's elements (MinDistortion tables)
+            const uint64_t *q = (const uint64_t *)(vcl + (size_t)m.vrow * v);
+            bool uni = true;
+            for (int j = 1; j < m.cnt && uni; ++j) uni = std::memcmp(q, q + (size_t)j * v, sizeof(double) * v) == 0;
+            if (uni) m.flags |= MF_VUNI;
+        }
         if (kind == QPD_FASTSCL_LUT && OP_R0 + t == OP_R1 && m.cnt <= 32) {
             m.tab = (int)r1tab.size();  // rank-key table of this node
             r1_rank_table(r1tab, vcl, N, v, d, node);
@@ -503,6 +509,9 @@ const void *fast_kernel(int kind, int sets, bool l8) {
         case QPD_SC_LUT: return sets == 2 ? QPD_FK(K_SC_LUT, 2, false) : QPD_FK(K_SC_LUT, 1, false);
         case QPD_FASTSC_LUT: return sets == 2 ? QPD_FK(K_FASTSC_LUT, 2, false) : QPD_FK(K_FASTSC_LUT, 1, false);
         case QPD_SCL_LUT:
+#ifdef QPD_SETS3
+            if (sets == 3 && l8) return QPD_FK(K_SCL_LUT, 3, true);
+#endif
             if (sets == 2) return l8 ? QPD_FK(K_SCL_LUT, 2, true) : QPD_FK(K_SCL_LUT, 2, false);
             return l8 ? QPD_FK(K_SCL_LUT, 1, true) : QPD_FK(K_SCL_LUT, 1, false);
         case QPD_FASTSCL_LUT:
@@ -562,6 +571,9 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     };
     d->sets = c->kind == QPD_FASTSCL_LUT ? 1 : kDefaultSets;  // FastSCL's R1 argsort state spills at NS = 2
     if (const char *e = getenv("QPD_SETS")) d->sets = std::min(2, std::max(1, atoi(e)));
+#ifdef QPD_SETS3
+    if (const char *e = getenv("QPD_SETS")) if (atoi(e) == 3 && c->kind == QPD_SCL_LUT && d->L == 8) d->sets = 3;
+#endif
     d->l8 = (c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT) && d->L == 8;
     const int NS = d->sets;
     FastLayout Ly;
@@ -604,7 +616,7 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     }
     // LDS per wave = NS * (selection scratch + rows of depths >= D); the budget
     // is measured: occupancy beats LDS residency of the shallow depths.
-    int budget = NS == 1 ? 6 * 1024 : 10 * 1024;
+    int budget = NS == 1 ? 6 * 1024 : NS == 2 ? 10 * 1024 : 15 * 1024;
     if (const char *e = getenv("QPD_LDS_BUDGET")) budget = atoi(e);
     while (Ly.D <= n && NS * (qpd::kSelInts * 4 + lds_rows(Ly.D) * 256) > budget) ++Ly.D;
     F.lds_from = Ly.D;

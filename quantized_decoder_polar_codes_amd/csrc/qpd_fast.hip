@@ -47,6 +47,8 @@ enum MopFlag : int32_t {
     MF_BFG = 1024,    // BOT3 whose 8 input symbols are f (or g, MF_BG) of its depth n-4 parent's 16:
     MF_BG = 2048,     //   the parent's F / G op folded in (src = S[n-4], table at tab2, U[n-3] at u_row)
     MF_BCOMB = 4096,  // right BOT3 that also runs its parent's combine (dst = U/R[n-4])
+    MF_VUNI = 8192,   // special node whose elements share one quanta row (v <= 16): quanta and
+                      //   R1 ranks are looked up in a register row instead of gathered per element
 };
 
 struct MOp {
@@ -274,7 +276,7 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
     const bool dl = DL >= 0 ? DL != 0 : (op.flags & MF_DST_LDS) != 0, ul = op.flags & MF_U_LDS;
     if (ctemp >= 64) {
         const int nwo = ctemp >> 3;  // multiple of 8
-        if constexpr (NS == 2) {
+        if constexpr (NS >= 2) {
             // chunks of 4 words of both sets: the sets' loads are in flight together
             for (int w0 = 0; w0 < nwo; w0 += 4) {
                 uint32_t A[NS][4], B[NS][4], ub[NS];
@@ -489,13 +491,37 @@ __device__ __forceinline__ uint32_t leaf_fork(Path &st, double dm, int gl, int g
         // their bits.  v_max_f64 by inline asm: the builtin would canonicalize the
         // DPP results first (two more VALU per step).
         const uint64_t K = __builtin_bit_cast(uint64_t, st.pm), F = __builtin_bit_cast(uint64_t, kf);
+#ifdef QPD_FAST_HI
+        // Conservative 32-bit form: hi(F) > max hi(K) implies F > every keep;
+        // an undecided case (equal high words: +inf or |dm| below 2^-20 of pm)
+        // takes the full selection, which is always exact.
+        const uint32_t kh = (uint32_t)(K >> 32), fh = (uint32_t)(F >> 32);
+        uint32_t mh = kh;
+        mh = max(mh, (uint32_t)__builtin_amdgcn_mov_dpp((int)mh, kDppXor1, 0xF, 0xF, true));
+        mh = max(mh, (uint32_t)__builtin_amdgcn_mov_dpp((int)mh, kDppXor2, 0xF, 0xF, true));
+        mh = max(mh, (uint32_t)__builtin_amdgcn_mov_dpp((int)mh, kDppHalfMirror, 0xF, 0xF, true));
+        const uint64_t Kn = dpp64<kDppRowShl1>(K);  // pm of slot gl+1
+        // lane masks straight from the compares (no ballot materialization)
+        const uint64_t okm = __builtin_amdgcn_uicmp(fh, mh, 34 /* ugt */) &
+                             (__builtin_amdgcn_uicmp((uint32_t)gl, 7u, 32 /* eq */) |
+                              __builtin_amdgcn_uicmpl(K, Kn, 37 /* ule */));
+        if (okm == ~0ull) return hd;
+#else
         uint64_t mk = K;
         mk = dmax_bits(mk, dpp64<kDppXor1>(mk));
         mk = dmax_bits(mk, dpp64<kDppXor2>(mk));
         mk = dmax_bits(mk, dpp64<kDppHalfMirror>(mk));  // lane i^7 lies in the other quad
         const uint64_t Kn = dpp64<kDppRowShl1>(K);  // pm of slot gl+1
+#ifdef QPD_FAST_MASK
+        const uint64_t okm = __builtin_amdgcn_uicmpl(F, mk, 35 /* uge */) &
+                             (__builtin_amdgcn_uicmp((uint32_t)gl, 7u, 32 /* eq */) |
+                              __builtin_amdgcn_uicmpl(K, Kn, 37 /* ule */));
+        if (okm == ~0ull) return hd;
+#else
         const bool ok = F >= mk && (gl == 7 || K <= Kn);
         if (__ballot(ok) == ~0ull) return hd;
+#endif
+#endif
     }
 #endif
     const Sel sl = L8 ? select_survivors8(st.pm, kf, gl, gbase, lane, sel) : select_survivors(st.pm, kf, gl, gbase, L, sel);
@@ -529,6 +555,49 @@ __device__ __forceinline__ void leaf_decide(Path (&st)[NS], const double (&dm)[N
         }
         return;
     }
+#if defined(QPD_ILV) && !defined(QPD_NO_FASTKEEP)
+    if constexpr (L8 && NS > 1) {
+        // All sets in one straight-line block: the identity checks of every set,
+        // one wave-uniform branch, then (if any set needs it) the selections and
+        // fork shuffles of every set interleaved.  Forking set by set behind a
+        // branch each would serialize the sets' dependency chains.  A set whose
+        // identity check holds gets the identity from the full selection too.
+        double kf[NS];
+        uint32_t hd[NS];
+        bool fast = true;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            kf[s] = st[s].pm + fabs(dm[s]);
+            hd[s] = dm[s] < 0;  // H4: SCL family `< 0`
+            const uint64_t K = __builtin_bit_cast(uint64_t, st[s].pm), F = __builtin_bit_cast(uint64_t, kf[s]);
+            uint64_t mk = K;
+            mk = dmax_bits(mk, dpp64<kDppXor1>(mk));
+            mk = dmax_bits(mk, dpp64<kDppXor2>(mk));
+            mk = dmax_bits(mk, dpp64<kDppHalfMirror>(mk));
+            const uint64_t Kn = dpp64<kDppRowShl1>(K);
+            fast = fast && __ballot(F >= mk && (gl == 7 || K <= Kn)) == ~0ull;
+        }
+        if (fast) {
+#pragma unroll
+            for (int s = 0; s < NS; ++s) dec[s] = hd[s];
+            return;
+        }
+        Sel sl[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) sl[s] = select_survivors8(st[s].pm, kf[s], gl, gbase, lane, sel + sstride * s);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const int p = gbase + sl[s].parent;
+            dec[s] = (uint32_t)__shfl((int)hd[s], p) ^ (sl[s].upper ? 1u : 0u);
+            st[s].pm = pick(sl[s].upper, shfld(kf[s], p), shfld(st[s].pm, p));
+            st[s].ps = shfl64(st[s].ps, p);
+            st[s].pu = shfl64(st[s].pu, p);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) extra[s][i] = (uint32_t)__shfl((int)extra[s][i], p);
+        }
+        return;
+    }
+#endif
 #pragma unroll
     for (int s = 0; s < NS; ++s) dec[s] = leaf_fork<L8>(st[s], dm[s], gl, gbase, L, lane, sel + sstride * s, extra[s]);
 }
@@ -555,6 +624,44 @@ __device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], u
                                          uint32_t (&c)[NS]) {
     double dm[NS];
     uint32_t bl[NS], br[NS];
+#ifdef QPD_SPEC_R
+    if (kList && !(fr & 1)) {
+        // Info left leaf: the right leaf's quanta for both of its possible
+        // left decisions are looked up before the fork (they depend only on the
+        // lineage's W1), follow the surviving lineage through the fork, and
+        // the decision then selects one -- the right leaf's two dependent LDS
+        // lookups leave the fork-to-fork critical path.
+        uint32_t xx[NS][6];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const uint32_t a = (x[s][1] >> 16) & 15u, b = (x[s][1] >> 20) & 15u, ab = (a << 4) | b;
+            dm[s] = shfld(V, vo + (int)lut4(Tf, ab + fo));
+            const double r0 = shfld(V, vo + 16 + (int)lut4(Tg, ab)), r1 = shfld(V, vo + 16 + (int)lut4(Tg, 256u | ab));
+            const uint64_t b0 = __builtin_bit_cast(uint64_t, r0), b1 = __builtin_bit_cast(uint64_t, r1);
+            xx[s][0] = x[s][0];
+            xx[s][1] = x[s][1];
+            xx[s][2] = (uint32_t)b0;
+            xx[s][3] = (uint32_t)(b0 >> 32);
+            xx[s][4] = (uint32_t)b1;
+            xx[s][5] = (uint32_t)(b1 >> 32);
+        }
+        leaf_decide<kList, L8>(st, dm, false, gl, gbase, L, lane, sel, sstride, xx, bl);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            x[s][0] = xx[s][0];
+            x[s][1] = (xx[s][1] & ~(1u << 24)) | (bl[s] << 24);
+            const uint64_t r = bl[s] ? ((uint64_t)xx[s][5] << 32 | xx[s][4]) : ((uint64_t)xx[s][3] << 32 | xx[s][2]);
+            dm[s] = __builtin_bit_cast(double, r);
+        }
+        leaf_decide<kList, L8>(st, dm, fr & 2, gl, gbase, L, lane, sel, sstride, x, br);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const uint32_t bl2 = (x[s][1] >> 24) & 1u;
+            c[s] = (bl2 ^ br[s]) | (br[s] << 1);
+        }
+        return;
+    }
+#endif
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const uint32_t a = (x[s][1] >> 16) & 15u, b = (x[s][1] >> 20) & 15u;
@@ -722,6 +829,14 @@ __device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const 
     const int m = (L - 1) < temp ? (L - 1) : temp;
     const uint16_t *rk = P.r1_rank + op.tab;
     const double *vq = P.vcl + (size_t)op.vrow * v;
+    // MF_VUNI: one quanta row and one rank row for all elements, in registers
+    const bool uni = op.flags & MF_VUNI;
+    const int s16 = lane & 15;
+    const uint32_t rrow = uni && s16 < v ? (uint32_t)rk[s16] : 0u;
+    const double vrow = uni && s16 < v ? vq[s16] : 0.0;
+    auto rank_of = [&](int j, uint32_t sym) -> uint32_t {
+        return uni ? (uint32_t)__shfl((int)rrow, (int)sym) : (uint32_t)rk[j * v + sym];
+    };
     uint32_t W[4], hw = 0;
 #pragma unroll
     for (int w = 0; w < 4; ++w) W[w] = (8 * w < temp) ? M.ld(sl, op.src_row + w, src) : 0u;
@@ -734,7 +849,7 @@ __device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const 
         for (int j = 0; j < 16; ++j) {
             ent[j] = 0xffffffffu;
             if (j < temp) {
-                const uint32_t e = rk[j * v + ((W[j >> 3] >> (4 * (j & 7))) & 15u)];
+                const uint32_t e = rank_of(j, (W[j >> 3] >> (4 * (j & 7))) & 15u);
                 hw |= (e & 1u) << j;
                 ent[j] = ((e >> 1) << 5) | (uint32_t)j;
             }
@@ -755,7 +870,7 @@ __device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const 
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
             if (j < temp) {
-                const uint32_t e = rk[j * v + ((W[j >> 3] >> (4 * (j & 7))) & 15u)];
+                const uint32_t e = rank_of(j, (W[j >> 3] >> (4 * (j & 7))) & 15u);
                 hw |= (e & 1u) << j;
                 seq.set(j, (int)(((e >> 1) << 5) | (uint32_t)j));
             }
@@ -772,7 +887,8 @@ __device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const 
         if (q < m) {
             const int k = ord[q] >> 3;
             const uint32_t w = k == 0 ? W[0] : k == 1 ? W[1] : k == 2 ? W[2] : W[3];
-            ms[q] = fabs(vq[(size_t)ord[q] * v + ((w >> (4 * (ord[q] & 7))) & 15u)]);
+            const uint32_t sym = (w >> (4 * (ord[q] & 7))) & 15u;
+            ms[q] = fabs(uni ? shfld(vrow, (int)sym) : vq[(size_t)ord[q] * v + sym]);
         }
     }
     const uint32_t word = r1_layers<L8>(st, sel, gl, gbase, lane, L, m, ord, ms, hw, temp);
@@ -859,12 +975,20 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
     const int nwo = (temp + 31) >> 5;
     const int v = P.v;
     const double *vq = P.vcl + (size_t)op.vrow * v;  // row d-1, position temp*node
+    // MF_VUNI: the node's one quanta row, entry s in lanes s, s+16, s+32, s+48
+    const bool uni = fl & MF_VUNI;
+    const double vr = uni && (lane & 15) < v ? vq[lane & 15] : 0.0;
     // elements [8w, 8w + 8) of the node: quanta of its symbols
     auto llr8 = [&](int w, double (&l)[8], uint32_t &word) {
         word = M.ld(sl, op.src_row + w, src);
+        if (uni) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-            l[i] = (8 * w + i < temp) ? vq[(size_t)(8 * w + i) * v + ((word >> (4 * i)) & 15u)] : 0.0;
+            for (int i = 0; i < 8; ++i) l[i] = shfld(vr, (int)((word >> (4 * i)) & 15u));
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                l[i] = (8 * w + i < temp) ? vq[(size_t)(8 * w + i) * v + ((word >> (4 * i)) & 15u)] : 0.0;
+        }
     };
     const int n8 = (temp + 7) >> 3;
     if (op.type == OP_R0) {
@@ -985,6 +1109,9 @@ __device__ unsigned long long qpd_stamp_acc[64];
 #ifndef QPD_WPE2
 #define QPD_WPE2 4
 #endif
+#ifndef QPD_WPE3
+#define QPD_WPE3 3
+#endif
 // NS frame sets per wave (see above); L8: list decoders with L = 8.
 // LDS: NS * kSelInts ints of selection scratch, then NS * lds_rows rows.
 // Global slab: NS * glb_rows rows per workgroup.
@@ -992,7 +1119,7 @@ template <int KIND, int NS, bool L8>
 // `ops` is its own __restrict__ argument (= P.ops) so that the compiler can
 // prove the op records are never written and fetch them with scalar loads
 // instead of vector loads + readfirstlane, which drain vmcnt at every op.
-__global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QPD_WPE_FSCL : QPD_WPE1) void lut_fast_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
+__global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QPD_WPE_FSCL : QPD_WPE1) void lut_fast_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
                                                                uint8_t *__restrict__ out,
                                                                const MOp *__restrict__ ops) {
     constexpr bool kList = (KIND == K_SCL_LUT || KIND == K_FASTSCL_LUT);
@@ -1068,10 +1195,15 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QP
             const int fl = op.flags;
             switch (op.type) {
                 case OP_BOT3:
+#ifndef QPD_EXP_NO_BOT3  // register-pressure experiments only (wrong results)
                     bot3_op<kList, L8>(P, Mv, op, yv, stv, cur.T, cur.T2, gl, gbase, L, sel_all, sstride, lane);
+#endif
                     break;
                 case OP_F:
                 case OP_G: {
+#ifdef QPD_EXP_NO_FG
+                    break;
+#endif
                     int src[NS], usrc[NS];
 #pragma unroll
                     for (int s = 0; s < NS; ++s) {
@@ -1080,7 +1212,7 @@ __global__ __launch_bounds__(64, NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QP
                     }
                     if (fl & MF_GSEL)
                         gsel_op(Mv, op, yv, usrc, lane);
-                    else if (NS == 2 && !(fl & (MF_CHAN | MF_PRE))) {  // (one-set FastSCL: smaller code measured faster)
+                    else if (NS >= 2 && !(fl & (MF_CHAN | MF_PRE))) {  // (one-set FastSCL: smaller code measured faster)
                         // row spaces of source and destination fixed per instantiation
                         const int key = ((fl & MF_SRC_LDS) ? 1 : 0) | ((fl & MF_DST_LDS) ? 2 : 0);
 #define QPD_FG(G, S_, D_) fg_op<G, true, NS, S_, D_>(P, Mv, op, yv, src, usrc, cur.T, lane)

@@ -14,7 +14,8 @@ import bench  # noqa: E402
 kinds = sys.argv[1:] or ["SCL-LUT", "FastSCL-LUT"]
 F = int(os.environ.get("AB_FRAMES", "262144"))
 for kind in kinds:
-    d, _, _, _, _, sym = bench.workload(1024, 512, 8, kind, F, 2.0)
+    wl = bench.workload(1024, 512, 8, kind, F, 2.0)
+    d, sym = wl.dec, wl.sym
     out = d.decode_batch(sym)
     torch.cuda.synchronize()
     dig = hashlib.sha1(out.cpu().numpy().tobytes()).hexdigest()[:12]

@@ -23,9 +23,11 @@ buf = (ctypes.c_ulonglong * 64)()
 lib.qpd_debug_sel_stats(buf)
 cases = [("random 3..12", torch.from_numpy(np.random.default_rng(0).integers(3, 13, size=(F, N), dtype=np.int32)).cuda())]
 for eb in (1.0, 2.0, 3.0):
-    cases.append((f"AWGN {eb} dB", bench.workload(N, K, L, "SCL-LUT", F, eb, "minsum")[5]))
+    cases.append((f"AWGN {eb} dB", bench.workload(N, K, L, "SCL-LUT", F, eb, "minsum").sym))
+wl = bench.workload(N, K, L, "SCL-LUT", F, 2.0)  # the bench workload: MinDistortion tables, 2 dB
+cases.append(("bench (MinDistortion, 2 dB)", wl.sym))
 for kind, sym in cases:
-    d.decode_batch(sym)
+    (wl.dec if kind.startswith("bench") else d).decode_batch(sym)
     torch.cuda.synchronize()
     lib.qpd_debug_sel_stats(buf)
     a = np.array(buf[:], dtype=np.float64).reshape(8, 8).sum(axis=0)

@@ -17,7 +17,8 @@ N, K, L, F = (int(x) for x in sys.argv[2:6]) if len(sys.argv) > 5 else (1024, 51
 names = ["F", "G", "LEAF_L", "LEAF_R", "COMB", "R0", "R1", "REP", "SPC", "BOT3"]
 import bench  # noqa: E402
 
-d, _, fm, nt, _, sym = bench.workload(N, K, L, kind, F, 2.0)  # the bench workload (MinDistortion, 2 dB)
+_wl = bench.workload(N, K, L, kind, F, 2.0)  # the bench workload (MinDistortion, 2 dB)
+d, fm, nt, sym = _wl.dec, _wl.fm, _wl.nt, _wl.sym
 lib = _lib.load()
 buf = (ctypes.c_ulonglong * 64)()
 d.decode_batch(sym)

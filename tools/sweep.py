@@ -22,8 +22,9 @@ import bench  # noqa: E402
 
 # the bench's workload (MinDistortion tables and channel quantizer, GPU frames at Eb/N0 2 dB)
 maxF = max(frames_list)
-_, packed, fm, nt, _, sym = bench.workload(N, K, L, kind, maxF, float(os.environ.get("SWEEP_EBN0", "2.0")),
-                                           os.environ.get("SWEEP_LUTS", "mindistortion"))
+_wl = bench.workload(N, K, L, kind, maxF, float(os.environ.get("SWEEP_EBN0", "2.0")),
+                     os.environ.get("SWEEP_LUTS", "mindistortion"))
+packed, fm, nt, sym = _wl.packed, _wl.fm, _wl.nt, _wl.sym
 p = packed
 ref = None
 for budget, F, mw in itertools.product(budgets, frames_list, waves_list):
