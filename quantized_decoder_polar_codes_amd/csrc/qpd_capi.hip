@@ -113,6 +113,7 @@ struct qpd_decoder {
     DeviceBuf mc_pref, mc_crc;  // qpd_mc_frames: info bits before each word; CRC contribution per message bit
     int sets = 1;  // fast engine: frame sets per wave (lut_fast_kernel NS)
     bool l8 = false;  // fast engine: list decoder with L = 8 (select_survivors8)
+    bool r1l = false;  // fast engine: an R1 node needs r1_large (the R1L instantiation)
     bool pre = false;         // fast engine pre-mode: root_pre_kernel, then the decode on its rows
     int64_t pre_chunk = 0;    // frames per pre-pass chunk
     int64_t pre_cap = 0;      // frames pre_buf holds
@@ -501,10 +502,11 @@ void place_syncs(std::vector<qpd::MOp> &ops, bool list) {
 #endif
 constexpr int kDefaultSets = QPD_DEFAULT_SETS;
 
-// Instantiations of lut_fast_kernel<KIND, NS, L8>.
-const void *fast_kernel(int kind, int sets, bool l8) {
+// Instantiations of lut_fast_kernel<KIND, NS, L8, R1L>.
+const void *fast_kernel(int kind, int sets, bool l8, bool r1l) {
     using namespace qpd;
 #define QPD_FK(K, S, E) reinterpret_cast<const void *>(&lut_fast_kernel<K, S, E>)
+#define QPD_FKR(S, E) reinterpret_cast<const void *>(&lut_fast_kernel<K_FASTSCL_LUT, S, E, true>)
     switch (kind) {
         case QPD_SC_LUT: return sets == 2 ? QPD_FK(K_SC_LUT, 2, false) : QPD_FK(K_SC_LUT, 1, false);
         case QPD_FASTSC_LUT: return sets == 2 ? QPD_FK(K_FASTSC_LUT, 2, false) : QPD_FK(K_FASTSC_LUT, 1, false);
@@ -515,10 +517,15 @@ const void *fast_kernel(int kind, int sets, bool l8) {
             if (sets == 2) return l8 ? QPD_FK(K_SCL_LUT, 2, true) : QPD_FK(K_SCL_LUT, 2, false);
             return l8 ? QPD_FK(K_SCL_LUT, 1, true) : QPD_FK(K_SCL_LUT, 1, false);
         case QPD_FASTSCL_LUT:
+            if (r1l) {
+                if (sets == 2) return l8 ? QPD_FKR(2, true) : QPD_FKR(2, false);
+                return l8 ? QPD_FKR(1, true) : QPD_FKR(1, false);
+            }
             if (sets == 2) return l8 ? QPD_FK(K_FASTSCL_LUT, 2, true) : QPD_FK(K_FASTSCL_LUT, 2, false);
             return l8 ? QPD_FK(K_FASTSCL_LUT, 1, true) : QPD_FK(K_FASTSCL_LUT, 1, false);
         default: return nullptr;
     }
+#undef QPD_FKR
 #undef QPD_FK
 }
 
@@ -649,6 +656,9 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     }
     F.r1_rank = (const uint16_t *)d->r1_rank.p;
     place_syncs(mops, c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT);
+    for (const qpd::MOp &m : mops)  // R1 nodes the register/LDS argsort cannot take
+        if (c->kind == QPD_FASTSCL_LUT && m.type == qpd::OP_R1 && m.cnt > qpd::stl::kThreshold && !(m.flags & qpd::MF_R1_LDS))
+            d->r1l = true;
     F.nops = (int)mops.size();
     d->num_mops = F.nops;
     {
@@ -683,7 +693,7 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         const hipError_t oe =
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fast_kernel(d->kind, d->sets, d->l8), 64, d->lds_bytes);
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fast_kernel(d->kind, d->sets, d->l8, d->r1l), 64, d->lds_bytes);
         if (oe != hipSuccess || per_cu <= 0) per_cu = 16;
         mw = std::max(1, ncu) * per_cu;
     }
@@ -984,7 +994,7 @@ int qpd_decode(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_o
         const size_t lds = (size_t)d->lds_bytes;
         qpd::FastPlan fp = d->fplan;
         fp.in_vec = ((uintptr_t)d_symbols & 15u) == 0 && (fp.N & 3) == 0;
-        const void *kfn = fast_kernel(d->kind, d->sets, d->l8);
+        const void *kfn = fast_kernel(d->kind, d->sets, d->l8, d->r1l);
         if (!kfn) return fail(QPD_E_INVALID, "bad kind");
         auto decode = [&](const int32_t *in_arg, int64_t Bc, uint8_t *out_arg) -> int {
             const int64_t fgroups = (Bc + tw - 1) / tw;

@@ -965,7 +965,11 @@ __device__ __forceinline__ void r1_large(const FastPlan &P, const Mem &M, const 
     }
 }
 
-template <bool kList, bool L8>
+// R1L: the schedule has an R1 node that needs r1_large (> 32 elements, or > 16
+// without LDS room; N >= 2048 codes).  Only those plans get it compiled in:
+// its argsort stack and arrays cost the other instantiations registers and
+// scratch (+3 % FastSCL-LUT at N = 1024 without it).
+template <bool kList, bool L8, bool R1L>
 __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, const MOp &op, Path &st, int *sel, int gl,
                                            int gbase, int L, int lane) {
     const int fl = op.flags;
@@ -1085,7 +1089,7 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
         }
     } else if (temp <= stl::kThreshold || (fl & MF_R1_LDS)) {
         r1_small<L8>(P, M, op, st, sel, gl, gbase, L, lane, temp);
-    } else {
+    } else if constexpr (R1L) {
         r1_large(P, M, op, st, sel, gl, gbase, L, lane, temp);
     }
     if (!(fl & MF_TO_R)) st.pu = pset(st.pu, op.sh_dst, gl);
@@ -1115,7 +1119,7 @@ __device__ unsigned long long qpd_stamp_acc[64];
 // NS frame sets per wave (see above); L8: list decoders with L = 8.
 // LDS: NS * kSelInts ints of selection scratch, then NS * lds_rows rows.
 // Global slab: NS * glb_rows rows per workgroup.
-template <int KIND, int NS, bool L8>
+template <int KIND, int NS, bool L8, bool R1L = false>
 // `ops` is its own __restrict__ argument (= P.ops) so that the compiler can
 // prove the op records are never written and fetch them with scalar loads
 // instead of vector loads + readfirstlane, which drain vmcnt at every op.
@@ -1314,7 +1318,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
                     Path &st = stv[s];
                     const Mem &M = Mv[s];
                     int *const sel = sel_all + sstride * s;
-                    special_op<kList, L8>(P, M, op, st, sel, gl, gbase, L, lane);
+                    special_op<kList, L8, R1L>(P, M, op, st, sel, gl, gbase, L, lane);
                   }
                   break;
                 }
