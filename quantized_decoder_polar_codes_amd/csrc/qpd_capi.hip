@@ -128,10 +128,17 @@ struct qpd_decoder {
     // staging for the host-buffer entry points
     DeviceBuf h_in, h_out;
     size_t h_in_bytes = 0, h_out_bytes = 0;
+    // host-buffer entry points: own stream and a pinned staging buffer (one
+    // stream synchronization per call: copy in, decode, copy out + error word)
+    hipStream_t hs = nullptr;
+    void *pin = nullptr;
+    size_t pin_bytes = 0;
     // qpd_profile: HIP events around every launch, per kernel class
     bool prof = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[QPD_KC_COUNT];
     ~qpd_decoder() {
+        if (hs) (void)hipStreamDestroy(hs);
+        if (pin) (void)hipHostFree(pin);
         for (auto &v : prof_ev)
             for (auto &e : v) {
                 (void)hipEventDestroy(e.first);
@@ -1059,23 +1066,15 @@ int qpd_decode_f64(qpd_decoder *d, const double *d_llr, int64_t B, uint8_t *d_ou
     return launch_generic(d, d_llr, B, d_out, grid, (hipStream_t)stream);
 }
 
-int qpd_check_input_error(qpd_decoder *d) {
-    if (!d) return fail(QPD_E_INVALID, "null decoder");
-    int rc = set_device(d);
-    if (rc) return rc;
-    int32_t flag = 0;
-    QPD_HIP(hipDeviceSynchronize());
-    QPD_HIP(hipMemcpy(&flag, d->err.p, sizeof(flag), hipMemcpyDeviceToHost));
-    if (flag) {
-        QPD_HIP(hipMemset(d->err.p, 0, sizeof(int32_t)));
-        std::string msg;
-        if (flag & qpd::ERR_SYMBOL) msg += "channel symbol outside [0, v) in decoder input; ";
-        if (flag & qpd::ERR_LLOYD) msg += "Lloyd bisect index outside the reconstruction list (reference UB); ";
-        if (flag & qpd::ERR_NAN_PM) msg += "NaN path metric reached the list sort (reference UB); ";
-        msg.resize(msg.size() - 2);
-        return fail(QPD_E_INPUT, msg);
-    }
-    return QPD_OK;
+}  // extern "C"
+
+static int input_error(int32_t flag) {
+    std::string msg;
+    if (flag & qpd::ERR_SYMBOL) msg += "channel symbol outside [0, v) in decoder input; ";
+    if (flag & qpd::ERR_LLOYD) msg += "Lloyd bisect index outside the reconstruction list (reference UB); ";
+    if (flag & qpd::ERR_NAN_PM) msg += "NaN path metric reached the list sort (reference UB); ";
+    msg.resize(msg.size() - 2);
+    return fail(QPD_E_INPUT, msg);
 }
 
 static int ensure(DeviceBuf &b, size_t &have, size_t need) {
@@ -1089,32 +1088,77 @@ static int ensure(DeviceBuf &b, size_t &have, size_t need) {
     return QPD_OK;
 }
 
+// One synchronous host-buffer decode: input staged through pinned memory,
+// H2D copy, decode and D2H copies of the bits and the error word queued on
+// the handle's own stream, one stream synchronization.  (What a per-frame
+// decode(symbols) call of the reference drivers costs here: tools/latency.py.)
+template <class In, class Dec>
+static int host_roundtrip(qpd_decoder *d, const In *h_in, int64_t B, uint8_t *h_out, Dec dec) {
+    const size_t in_b = (size_t)B * d->N * sizeof(In), out_b = (size_t)B * d->out_bits;
+    const size_t out_at = (in_b + 15) & ~(size_t)15, err_at = out_at + ((out_b + 15) & ~(size_t)15);
+    int rc = ensure(d->h_in, d->h_in_bytes, in_b);
+    if (rc) return rc;
+    if ((rc = ensure(d->h_out, d->h_out_bytes, std::max<size_t>(1, out_b)))) return rc;
+    if (!d->hs) QPD_HIP(hipStreamCreateWithFlags(&d->hs, hipStreamNonBlocking));
+    if (d->pin_bytes < err_at + 16) {
+        if (d->pin) QPD_HIP(hipHostFree(d->pin));
+        d->pin = nullptr;
+        d->pin_bytes = 0;
+        QPD_HIP(hipHostMalloc(&d->pin, err_at + 16, hipHostMallocDefault));
+        d->pin_bytes = err_at + 16;
+    }
+    char *pin = (char *)d->pin;
+    std::memcpy(pin, h_in, in_b);
+    QPD_HIP(hipMemcpyAsync(d->h_in.p, pin, in_b, hipMemcpyHostToDevice, d->hs));
+    if ((rc = dec((const In *)d->h_in.p, (uint8_t *)d->h_out.p, d->hs))) return rc;
+    if (out_b) QPD_HIP(hipMemcpyAsync(pin + out_at, d->h_out.p, out_b, hipMemcpyDeviceToHost, d->hs));
+    QPD_HIP(hipMemcpyAsync(pin + err_at, d->err.p, sizeof(int32_t), hipMemcpyDeviceToHost, d->hs));
+    QPD_HIP(hipStreamSynchronize(d->hs));
+    std::memcpy(h_out, pin + out_at, out_b);
+    int32_t flag = 0;
+    std::memcpy(&flag, pin + err_at, sizeof(flag));
+    if (flag) {
+        QPD_HIP(hipMemsetAsync(d->err.p, 0, sizeof(int32_t), d->hs));
+        QPD_HIP(hipStreamSynchronize(d->hs));
+        return input_error(flag);
+    }
+    return QPD_OK;
+}
+
+extern "C" {
+
+int qpd_check_input_error(qpd_decoder *d) {
+    if (!d) return fail(QPD_E_INVALID, "null decoder");
+    int rc = set_device(d);
+    if (rc) return rc;
+    int32_t flag = 0;
+    QPD_HIP(hipDeviceSynchronize());
+    QPD_HIP(hipMemcpy(&flag, d->err.p, sizeof(flag), hipMemcpyDeviceToHost));
+    if (flag) {
+        QPD_HIP(hipMemset(d->err.p, 0, sizeof(int32_t)));
+        return input_error(flag);
+    }
+    return QPD_OK;
+}
+
 int qpd_decode_host(qpd_decoder *d, const int32_t *h_symbols, int64_t B, uint8_t *h_out) {
     if (!d) return fail(QPD_E_INVALID, "null decoder");
     if (B <= 0) return B == 0 ? QPD_OK : fail(QPD_E_INVALID, "negative batch");
+    if (!h_symbols || !h_out) return fail(QPD_E_INVALID, "null buffer");
     int rc = set_device(d);
     if (rc) return rc;
-    const size_t in_b = (size_t)B * d->N * sizeof(int32_t), out_b = (size_t)B * d->out_bits;
-    if ((rc = ensure(d->h_in, d->h_in_bytes, in_b))) return rc;
-    if ((rc = ensure(d->h_out, d->h_out_bytes, std::max<size_t>(1, out_b)))) return rc;
-    QPD_HIP(hipMemcpy(d->h_in.p, h_symbols, in_b, hipMemcpyHostToDevice));
-    if ((rc = qpd_decode(d, (const int32_t *)d->h_in.p, B, (uint8_t *)d->h_out.p, nullptr))) return rc;
-    if (out_b) QPD_HIP(hipMemcpy(h_out, d->h_out.p, out_b, hipMemcpyDeviceToHost));
-    return qpd_check_input_error(d);
+    return host_roundtrip(d, h_symbols, B, h_out,
+                          [&](const int32_t *in, uint8_t *out, hipStream_t st) { return qpd_decode(d, in, B, out, st); });
 }
 
 int qpd_decode_f64_host(qpd_decoder *d, const double *h_llr, int64_t B, uint8_t *h_out) {
     if (!d) return fail(QPD_E_INVALID, "null decoder");
     if (B <= 0) return B == 0 ? QPD_OK : fail(QPD_E_INVALID, "negative batch");
+    if (!h_llr || !h_out) return fail(QPD_E_INVALID, "null buffer");
     int rc = set_device(d);
     if (rc) return rc;
-    const size_t in_b = (size_t)B * d->N * sizeof(double), out_b = (size_t)B * d->out_bits;
-    if ((rc = ensure(d->h_in, d->h_in_bytes, in_b))) return rc;
-    if ((rc = ensure(d->h_out, d->h_out_bytes, std::max<size_t>(1, out_b)))) return rc;
-    QPD_HIP(hipMemcpy(d->h_in.p, h_llr, in_b, hipMemcpyHostToDevice));
-    if ((rc = qpd_decode_f64(d, (const double *)d->h_in.p, B, (uint8_t *)d->h_out.p, nullptr))) return rc;
-    if (out_b) QPD_HIP(hipMemcpy(h_out, d->h_out.p, out_b, hipMemcpyDeviceToHost));
-    return qpd_check_input_error(d);
+    return host_roundtrip(d, h_llr, B, h_out,
+                          [&](const double *in, uint8_t *out, hipStream_t st) { return qpd_decode_f64(d, in, B, out, st); });
 }
 
 int qpd_mc_frames(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64_t frame0, int64_t B, uint8_t *d_msg,
