@@ -172,7 +172,12 @@ class Ctx:
         if self.group is not None:
             import torch.distributed as dist
 
-            dist.all_reduce(t, op=op, group=self.group)
+            if dist.get_backend(self.group) == "gloo" and t.is_cuda:  # rehearsal runs: gloo reduces host tensors
+                h = t.cpu()
+                dist.all_reduce(h, op=op, group=self.group)
+                t.copy_(h)
+            else:
+                dist.all_reduce(t, op=op, group=self.group)
         return t
 
 
@@ -361,8 +366,9 @@ def mc_rank(args, ctx, wl):
     dec = wl.dec
     ctx.barrier()
     t0 = time.perf_counter()
+    gloo = ctx.group is not None and dist.get_backend(ctx.group) == "gloo"
     r = MC.run_point(wl.src, dec.decode_batch, dec.K, args.ebn0, args.frames, F, stop, A=dec.out_bits,
-                     group=ctx.group, count_device=ctx.device)
+                     group=ctx.group, count_device="cpu" if gloo else ctx.device)
     ctx.barrier()
     tmax = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=ctx.device)
     ctx.allreduce(tmax, dist.ReduceOp.MAX)
@@ -478,10 +484,15 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local if world > 1 else 0)
+    # Rehearsal of the N-rank path on fewer GPUs (tests of the launch and
+    # sharding on a one-GPU box): QPD_BENCH_DEVICES maps local ranks onto the
+    # listed devices, QPD_BENCH_BACKEND=gloo replaces RCCL (which refuses two
+    # ranks on one device).  Defaults: rank i on GPU i, RCCL.
+    devs = [int(x) for x in os.environ.get("QPD_BENCH_DEVICES", "").split(",") if x.strip()]
+    torch.cuda.set_device(devs[local % len(devs)] if devs else (local if world > 1 else 0))
     group = None
     if world > 1:
-        dist.init_process_group("nccl")  # RCCL over xGMI
+        dist.init_process_group(os.environ.get("QPD_BENCH_BACKEND", "nccl"))  # "nccl" = RCCL over xGMI
         group = dist.group.WORLD
     dev = torch.device("cuda", torch.cuda.current_device())
     ctx = Ctx(rank, world, dev, group)
