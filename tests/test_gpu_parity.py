@@ -389,3 +389,55 @@ def test_gpu_with_designed_tables_matches_oracle(kind, L, qpd, oracle_mod):
     got = qpd.from_packed(kind, d.packed(), K, fm, L=L, node_type=nt).decode_batch(sym)
     assert np.array_equal(got, want)
     assert (got != msg).any(1).mean() < 0.5
+
+
+def test_kernel_timing_and_lds_probe(qpd):
+    """The measurement hooks bench.py relies on: per-class launch timing
+    (HIP events on the launch stream) and the on-chip peak probe."""
+    import ctypes
+
+    import torch
+
+    from quantized_decoder_polar_codes_amd import _lib
+    from quantized_decoder_polar_codes_amd import lut as LU
+
+    N, K = 256, 128
+    fm, nt = _node_type(N, K)
+    dec = qpd.from_packed("SCL-LUT", LU.minsum_uniform_luts(N), K, fm, L=8)
+    sym = torch.randint(0, 16, (4096, N), dtype=torch.int32, device="cuda")
+    dec.profile(True)
+    for _ in range(3):
+        out = dec.decode_batch(sym)
+    kt = dec.kernel_times()
+    dec.profile(False)
+    assert kt["decode"][1] == 3 and kt["decode"][0] > 0
+    assert kt["pre"][1] == 3  # pre-mode at N >= 16
+    assert dec.kernel_times()["decode"][1] == 0  # read and forgotten
+    dec.decode_batch(sym)
+    assert dec.kernel_times()["decode"][1] == 0  # not recorded while disabled
+    assert torch.equal(out, dec.decode_batch(sym))
+    rates = {}
+    for op in (_lib.QPD_PROBE_BPERMUTE, _lib.QPD_PROBE_READ_B32, _lib.QPD_PROBE_READ_B64):
+        g = ctypes.c_double()
+        _lib.check(_lib.load().qpd_probe_lds(0, op, ctypes.byref(g)))
+        rates[op] = g.value
+    assert all(1e3 < r < 1e6 for r in rates.values())  # GB/s: between 1 TB/s and 1 PB/s
+    assert rates[_lib.QPD_PROBE_READ_B64] > rates[_lib.QPD_PROBE_BPERMUTE]
+
+
+def test_host_decode_reports_out_of_range_symbol(qpd):
+    """The per-frame host path (pinned staging, one stream sync) still raises on
+    a channel symbol outside [0, v) and recovers for the next call."""
+    from quantized_decoder_polar_codes_amd import lut as LU
+
+    N, K = 128, 64
+    fm, nt = _node_type(N, K)
+    dec = qpd.from_packed("SCL-LUT", LU.minsum_uniform_luts(N), K, fm, L=4)
+    good = np.random.default_rng(3).integers(0, 16, size=(5, N), dtype=np.int32)
+    bad = good.copy()
+    bad[2, 7] = 16
+    with pytest.raises(ValueError, match="outside"):
+        dec.decode_batch(bad)
+    a = dec.decode_batch(good)
+    b = np.stack([dec.decode(x) for x in good])
+    assert np.array_equal(a, b)
