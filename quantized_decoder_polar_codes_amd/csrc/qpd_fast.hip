@@ -781,24 +781,29 @@ struct LdsSeq16 {
 };
 
 // Survivor layers of an R1 node (FastSCLLUTDecoder.cpp:118-166) after its
-// argsort: ord[q] / ms[q] = element and magnitude of the q-th smallest |llr|,
-// hw = hard decisions (l < 0).  Each of the m layers forks on flipping the
-// next element; ord/ms/flips follow the surviving lineage, the flip position
-// is the slot's own pre-selection ord (H2).  Returns the node's bits.
-// The arrays never move: a slot's lineage holds the arrays its `origin` lane
-// computed (read per layer by two shuffles), and its flips are one bit mask
-// (temp <= 32) shuffled with the survivors -- 5 shuffles a layer, not ~27.
+// argsort: ord[q] = element of the q-th smallest |llr| (5 bits each in
+// ordp0 / ordp1) and its symbol (4 bits each in symp), hw = hard decisions
+// (l < 0).  Each of the m layers forks on flipping the next element; the flip
+// position is the slot's own pre-selection ord (H2).  The arrays never move: a
+// slot's lineage holds the arrays its `origin` lane computed (read per layer
+// by shuffles; each lane re-derives its own entry's magnitude, a quanta-row
+// lookup or a vcl read), and its flips are one bit mask (temp <= 32) shuffled
+// with the survivors.  Returns the node's bits.
 template <bool L8>
 __device__ __forceinline__ uint32_t r1_layers(Path &st, int *sel, int gl, int gbase, int lane, int L, int m,
-                                              const int (&ord)[kMaxM], const double (&ms)[kMaxM], uint32_t hw, int temp) {
+                                                     uint32_t ordp0, uint32_t ordp1, uint32_t symp, bool uni,
+                                                     double vrow, const double *vq, int v, uint32_t hw, int temp) {
     uint32_t flips = 0;
     int origin = gl;
 #pragma unroll
     for (int layer = 0; layer < kMaxM; ++layer) {
         if (layer < m) {
             const int o = gbase + origin;
-            const double kf = st.pm + shfld(ms[layer], o);
-            const int pos_old = __shfl(ord[layer], o);  // H2
+            const int own = (int)(layer < 6 ? __builtin_amdgcn_ubfe(ordp0, 5 * layer, 5) : ordp1);
+            const uint32_t sym = __builtin_amdgcn_ubfe(symp, 4 * layer, 4);
+            const double own_ms = fabs(uni ? shfld(vrow, (int)sym) : vq[(size_t)own * v + sym]);
+            const double kf = st.pm + shfld(own_ms, o);
+            const int pos_old = __shfl(own, o);  // H2
             const Sel sl = L8 ? select_survivors8(st.pm, kf, gl, gbase, lane, sel)
                               : select_survivors(st.pm, kf, gl, gbase, L, sel);
             const int p = gbase + sl.parent;
@@ -813,13 +818,6 @@ __device__ __forceinline__ uint32_t r1_layers(Path &st, int *sel, int gl, int gb
     return temp < 32 ? word & ((1u << temp) - 1u) : word;
 }
 
-// R1 node of FastSCL-LUT with at most 32 elements (FastSCLLUTDecoder.cpp:99-166).
-// Argsort keys are the host-built ranks of |llr| (r1_rank: equal magnitudes,
-// equal ranks), so everything stays in registers / LDS:
-//   <= 16 elements: libstdc++ sorts by insertion (stable), i.e. by
-//     (rank, element): the m smallest 32-bit entries rank << 5 | element;
-//   17..32 elements: the exact introsort replay (stl::sort_small) on 16-bit
-//     entries in the free LDS tail (MF_R1_LDS; rows of depths > d).
 template <bool L8>
 __device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const MOp &op, Path &st, int *sel, int gl,
                                          int gbase, int L, int lane, int temp) {
@@ -844,25 +842,43 @@ __device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const 
 #pragma unroll
     for (int q = 0; q < kMaxM; ++q) ord[q] = 0;
     if (temp <= stl::kThreshold) {
-        uint32_t ent[16];
+        // entries rank << 5 | j (< 2^14) two per register; the m smallest by
+        // packed 16-bit min trees (v_pk_min_u16), the taken one set to 0xFFFF
+        typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+        u16x2 ep[8];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            ent[j] = 0xffffffffu;
-            if (j < temp) {
-                const uint32_t e = rank_of(j, (W[j >> 3] >> (4 * (j & 7))) & 15u);
-                hw |= (e & 1u) << j;
-                ent[j] = ((e >> 1) << 5) | (uint32_t)j;
+        for (int i = 0; i < 8; ++i) {
+            uint32_t lo = 0xffffu, hi = 0xffffu;
+            if (2 * i < temp) {
+                const uint32_t e = rank_of(2 * i, (W[i >> 2] >> (8 * (i & 3))) & 15u);
+                hw |= (e & 1u) << (2 * i);
+                lo = ((e >> 1) << 5) | (uint32_t)(2 * i);
             }
+            if (2 * i + 1 < temp) {
+                const uint32_t e = rank_of(2 * i + 1, (W[i >> 2] >> (8 * (i & 3) + 4)) & 15u);
+                hw |= (e & 1u) << (2 * i + 1);
+                hi = ((e >> 1) << 5) | (uint32_t)(2 * i + 1);
+            }
+            ep[i] = __builtin_bit_cast(u16x2, lo | (hi << 16));
         }
 #pragma unroll
         for (int q = 0; q < kMaxM; ++q) {
             if (q < m) {
-                uint32_t mn = ent[0];
-#pragma unroll
-                for (int j = 1; j < 16; ++j) mn = ent[j] < mn ? ent[j] : mn;
+                u16x2 a = __builtin_elementwise_min(__builtin_elementwise_min(ep[0], ep[1]),
+                                                    __builtin_elementwise_min(ep[2], ep[3]));
+                u16x2 b = __builtin_elementwise_min(__builtin_elementwise_min(ep[4], ep[5]),
+                                                    __builtin_elementwise_min(ep[6], ep[7]));
+                a = __builtin_elementwise_min(a, b);
+                const uint32_t mn = a.x < a.y ? a.x : a.y;
                 ord[q] = (int)(mn & 31u);
+                const u16x2 mm = {(unsigned short)mn, (unsigned short)mn};
+                const u16x2 one = {1, 1}, zero = {0, 0};
 #pragma unroll
-                for (int j = 0; j < 16; ++j) ent[j] = ent[j] == mn ? 0xffffffffu : ent[j];
+                for (int i = 0; i < 8; ++i) {
+                    const u16x2 d = ep[i] - mm;                                // 0 where taken (all entries >= mn)
+                    const u16x2 t = __builtin_elementwise_min(d, one) ^ one;   // 1 where taken
+                    ep[i] = ep[i] | (zero - t);                               // taken -> 0xFFFF
+                }
             }
         }
     } else {
@@ -880,18 +896,21 @@ __device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const 
         for (int q = 0; q < kMaxM; ++q)
             if (q < m) ord[q] = seq.get(q) & 31;
     }
-    double ms[kMaxM];
+    uint32_t ordp0 = 0, ordp1 = 0, symp = 0;
 #pragma unroll
     for (int q = 0; q < kMaxM; ++q) {
-        ms[q] = 0;
         if (q < m) {
             const int k = ord[q] >> 3;
             const uint32_t w = k == 0 ? W[0] : k == 1 ? W[1] : k == 2 ? W[2] : W[3];
-            const uint32_t sym = (w >> (4 * (ord[q] & 7))) & 15u;
-            ms[q] = fabs(uni ? shfld(vrow, (int)sym) : vq[(size_t)ord[q] * v + sym]);
+            symp |= ((w >> (4 * (ord[q] & 7))) & 15u) << (4 * q);
+            if (q < 6)
+                ordp0 |= (uint32_t)ord[q] << (5 * q);
+            else
+                ordp1 = (uint32_t)ord[q];
         }
     }
-    const uint32_t word = r1_layers<L8>(st, sel, gl, gbase, lane, L, m, ord, ms, hw, temp);
+    const uint32_t word =
+        r1_layers<L8>(st, sel, gl, gbase, lane, L, m, ordp0, ordp1, symp, uni, vrow, vq, v, hw, temp);
     M.st(op.flags & MF_DST_LDS, op.dst_row, lane, word);
 }
 
@@ -1199,15 +1218,10 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
             const int fl = op.flags;
             switch (op.type) {
                 case OP_BOT3:
-#ifndef QPD_EXP_NO_BOT3  // register-pressure experiments only (wrong results)
                     bot3_op<kList, L8>(P, Mv, op, yv, stv, cur.T, cur.T2, gl, gbase, L, sel_all, sstride, lane);
-#endif
                     break;
                 case OP_F:
                 case OP_G: {
-#ifdef QPD_EXP_NO_FG
-                    break;
-#endif
                     int src[NS], usrc[NS];
 #pragma unroll
                     for (int s = 0; s < NS; ++s) {
