@@ -120,7 +120,7 @@ struct qpd_decoder {
     DeviceBuf pre_buf;
     DevPlan plan{};
     qpd::FastPlan fplan{};
-    DeviceBuf f_tab, g_tab, fscratch, mops, r1_rank;
+    DeviceBuf f_tab, g_tab, fscratch, mops, r1_rank, task_ctr;
     int num_mops = 0;
     std::vector<Op> ops_host;
     DeviceBuf lut_f, f_base, lut_g, g_base, vcl, ops, info_pos, scratch, err;
@@ -715,6 +715,12 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     F.info_pos = (const int32_t *)d->info_pos.p;
     F.scratch = (uint32_t *)d->fscratch.p;
     F.err = (int32_t *)d->err.p;
+    {
+        const uint32_t zero[2] = {0u, 0u};  // task queue: [0] tasks taken, [1] waves done
+        rc = upload(d->task_ctr, zero, 2);
+        if (rc) return rc;
+    }
+    F.task_ctr = (uint32_t *)d->task_ctr.p;
     return QPD_OK;
 }
 
@@ -1006,9 +1012,11 @@ int qpd_decode(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_o
         auto decode = [&](const int32_t *in_arg, int64_t Bc, uint8_t *out_arg) -> int {
             const int64_t fgroups = (Bc + tw - 1) / tw;
             int fgrid = (int)std::min<int64_t>(fgroups, d->max_waves);
-            // even out the rounds of the grid-stride loop (no partial last round)
-            const int64_t rounds = (fgroups + fgrid - 1) / fgrid;
-            fgrid = (int)((fgroups + rounds - 1) / rounds);
+            if (!QPD_DYN) {
+                // even out the rounds of the grid-stride loop (no partial last round)
+                const int64_t rounds = (fgroups + fgrid - 1) / fgrid;
+                fgrid = (int)((fgroups + rounds - 1) / rounds);
+            }
             const qpd::MOp *ops_arg = fp.ops;
             void *args[] = {&fp, &in_arg, &Bc, &out_arg, &ops_arg};
             return timed_launch(d, QPD_KC_DECODE, st, [&]() -> int {

@@ -87,6 +87,7 @@ struct FastPlan {
     const uint16_t *r1_rank;      // FastSCL R1 (<= 32 elements): [temp][v] rank << 1 | sign, per node at op.tab
     uint32_t *scratch;            // [waves][glb_rows][64]
     int32_t *err;
+    uint32_t *task_ctr;           // QPD_DYN task queue: [0] tasks taken, [1] waves done (both 0 between launches)
 };
 
 // Timing experiments only (wrong results): 0 = every op reads node 0's
@@ -97,6 +98,17 @@ struct FastPlan {
 #ifndef QPD_EXP_SLABMUL
 #define QPD_EXP_SLABMUL 1
 #endif
+
+#ifndef QPD_DYN
+#define QPD_DYN 1  // tasks from a device queue (0: static grid-stride with evened rounds)
+#endif
+
+// One atomic per wave (lane 0, a vector atomic), the old value broadcast.
+__device__ __forceinline__ int64_t wave_take(uint32_t *ctr) {
+    uint32_t v = 0;
+    if (threadIdx.x == 0) v = atomicAdd(ctr, 1u);
+    return (int64_t)__builtin_amdgcn_readfirstlane(v);
+}
 
 #ifndef QPD_SLAB_AUX
 #define QPD_SLAB_AUX 0  // cache-policy bits of the slab's buffer ops (2 = nt)
@@ -1164,7 +1176,11 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
     const int64_t ntasks = (B + NS * fpw - 1) / (NS * fpw);
     const double kInf = __builtin_huge_val();
 
-    for (int64_t task = blockIdx.x; task < ntasks; task += gridDim.x) {
+    // Tasks: the first blockIdx.x, then (QPD_DYN) the next untaken one from
+    // the queue -- every SIMD stays busy to the end whatever the residency --
+    // or the grid-stride successor.
+    for (int64_t task = blockIdx.x; task < ntasks;
+         task = QPD_DYN ? (int64_t)gridDim.x + wave_take(P.task_ctr) : task + gridDim.x) {
         Path stv[NS];
         {
             const int lane = threadIdx.x, gl = lane & (gs - 1);
@@ -1472,6 +1488,12 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
             atomicAdd(&qpd_stamp_acc[32 + threadIdx.x], (unsigned long long)stamp_cnt);
         }
 #endif
+    }
+    // The queue drains only after every wave has taken its last (failed)
+    // task; the last wave out zeroes both counters for the next launch.
+    if (QPD_DYN && wave_take(P.task_ctr + 1) == gridDim.x - 1 && threadIdx.x == 0) {
+        atomicExch(P.task_ctr, 0u);
+        atomicExch(P.task_ctr + 1, 0u);
     }
 }
 
