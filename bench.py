@@ -63,7 +63,7 @@ def parse(argv=None):
     ap.add_argument("--N", type=int, default=1024)
     ap.add_argument("--K", type=int, default=512)
     ap.add_argument("--L", type=int, default=8)
-    ap.add_argument("--frames", type=int, default=1 << 18, help="frames per GPU per step")
+    ap.add_argument("--frames", type=int, default=1 << 21, help="frames per GPU per step (one decode launch: 2^21 x 4 KB int32 symbols = 8 GB resident)")
     ap.add_argument("--ebn0", type=float, default=2.0)
     ap.add_argument("--max-waves", type=int, default=0)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
@@ -258,7 +258,7 @@ def run_rank(args, ctx, wl):
                               "lds_from_depth": info["lds_from_depth"],
                               "waves": min(info["max_waves"], -(-frames // info["frames_per_wave"]))})
     if kt:
-        res["roofline"] = roofline(args, dec, kt, frames)
+        res["roofline"] = roofline(args, dec, kt, frames, args.steps + args.warmup)
     return res
 
 
@@ -271,10 +271,11 @@ def _counters(args, frames):
         return None
 
 
-def roofline(args, dec, kt, frames):
+def roofline(args, dec, kt, frames, calls):
     """Roofline of the dominant kernel (lut_fast_kernel; generic_decode_kernel
     on the generic engine).  achieved = SURVEY.md §8(d)'s algorithmic on-chip
-    bytes (L*N*log2 N LUT lookups x 4 B per frame) x frames per launch / the
+    bytes (L*N*log2 N LUT lookups x 4 B per frame) x frames per launch (a
+    call of `frames` frames is one launch per pre-pass chunk) / the
     kernel's average launch duration from the HIP events on its stream; peak =
     the ds_bpermute_b32 rate probed on this GPU now (qpd_probe_lds: the
     instruction of every table lookup).  `hbm` keeps the contract's HBM view of
@@ -286,7 +287,8 @@ def roofline(args, dec, kt, frames):
     dec_ms, n_dec = kt["decode"]
     pre_ms, n_pre = kt["pre"]
     k_ms = dec_ms / max(1, n_dec)
-    call_ms = (dec_ms + pre_ms) / max(1, n_dec)
+    call_ms = (dec_ms + pre_ms) / max(1, calls)
+    per_launch = frames * calls / max(1, n_dec)  # frames per decode launch
     n = int(np.log2(args.N))
     onchip_per_frame = args.L * args.N * n * ONCHIP_BYTES_PER_LOOKUP if "SCL" in args.kind else args.N * n * 4
     peaks = {}
@@ -296,15 +298,15 @@ def roofline(args, dec, kt, frames):
         _lib.check(_lib.load().qpd_probe_lds(dec.device, op, ctypes.byref(g)))
         peaks[name] = g.value
     peak = peaks["ds_bpermute_b32"]
-    achieved = onchip_per_frame * frames / (k_ms * 1e-3) / 1e9
+    achieved = onchip_per_frame * per_launch / (k_ms * 1e-3) / 1e9
     hbm_bytes = frames * (args.N * 4 + dec.out_bits)  # int32 symbols in, uint8 bits out
     rec = _counters(args, frames)
     kname = "lut_fast_kernel" if dec.info()["engine"] == 2 else "generic_decode_kernel"
     kc = (rec or {}).get("kernels", {}).get(kname, {})
     out = {"bound": "lds", "achieved": achieved, "peak": peak, "unit": "GB/s", "frac": achieved / peak,
            "traffic": kc.get("traffic"), "kernel": kname, "kernel_ms": k_ms, "launches": n_dec,
-           "algorithmic_bytes_per_launch": onchip_per_frame * frames,
-           "algorithmic": f"{onchip_per_frame} B/frame on-chip (SURVEY.md §8(d)) x {frames} frames per launch",
+           "algorithmic_bytes_per_launch": onchip_per_frame * per_launch,
+           "algorithmic": f"{onchip_per_frame} B/frame on-chip (SURVEY.md §8(d)) x {per_launch:.0f} frames per launch",
            "peak_probe": peaks, "lds_hit": kc.get("lds_hit"),
            "traffic_note": "HBM-side bytes per launch of this kernel, 2 x FETCH_SIZE + WRITE_SIZE from separate "
                            "rocprofv3 --pmc passes (profiles/counters.json via tools/counters.py)",

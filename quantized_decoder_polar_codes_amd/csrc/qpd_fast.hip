@@ -1133,13 +1133,14 @@ __device__ unsigned long long qpd_stamp_acc[64];
 #endif
 
 // Waves per SIMD the register allocation targets: 6 (80 VGPRs) for one
-// frame set, 4 (128 VGPRs) for two, 5 (96 VGPRs) for FastSCL's one set (its
-// R1 argsort state spills the main loop at 80) -- the measured optima on MI355X.
+// frame set, 4 (128 VGPRs) for two, 6 for FastSCL's one set too (its special
+// ops spill ~136 B at 80 VGPRs, yet with the task queue 6 waves beat 5 by 4%)
+// -- the measured optima on MI355X.
 #ifndef QPD_WPE1
 #define QPD_WPE1 6
 #endif
 #ifndef QPD_WPE_FSCL
-#define QPD_WPE_FSCL 5
+#define QPD_WPE_FSCL 6
 #endif
 #ifndef QPD_WPE2
 #define QPD_WPE2 4

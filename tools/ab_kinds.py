@@ -12,7 +12,7 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 kinds = sys.argv[1:] or ["SCL-LUT", "FastSCL-LUT"]
-F = int(os.environ.get("AB_FRAMES", "262144"))
+F = int(os.environ.get("AB_FRAMES", "1048576"))
 for kind in kinds:
     wl = bench.workload(1024, 512, 8, kind, F, 2.0)
     d, sym = wl.dec, wl.sym

@@ -38,5 +38,5 @@ python3 tools/counters.py $FR "$O"/fetch/fetch_counter_collection.csv "$O"/write
   > "$P/counters_summary.txt"
 cp profiles/counters.json "$P/counters.json"
 cp "$O"/kt/kt_kernel_stats.csv "$P/kernel_stats.csv"
-grep -v amdgpu.ids "$O/kt.log" | tail -1 > "$P/bench_under_rocprof.jsonl" || true
+grep '^{' "$O/kt.log" | tail -1 > "$P/bench_under_rocprof.jsonl" || true
 echo "profile $TAG done"
