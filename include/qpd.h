@@ -173,7 +173,10 @@ int qpd_create(const qpd_config *cfg, qpd_decoder **out);
 void qpd_destroy(qpd_decoder *dec);
 
 /* LUT kinds.  d_symbols: device int32 [B][N]; d_out: device uint8 [B][K]
- * ([B][A] for the CRC-aided kinds; qpd_info.out_bits). */
+ * ([B][A] for the CRC-aided kinds; qpd_info.out_bits).
+ * A decoder owns its work buffers (slab, pre-pass rows, task queue): calls on
+ * one decoder must be ordered (one stream at a time); use one decoder per
+ * concurrent stream. */
 int qpd_decode(qpd_decoder *dec, const int32_t *d_symbols, int64_t B, uint8_t *d_out, void *stream);
 /* float64-LLR kinds (QPD_SC_FLOAT, 7..14).  d_llr: device float64 [B][N];
  * d_out: device uint8 [B][K] ([B][A] for QPD_CASCL_FLOAT). */

@@ -946,6 +946,15 @@ int qpd_create(const qpd_config *cfg, qpd_decoder **out) {
     P.info_pos = (const int32_t *)d->info_pos.p;
     P.scratch = (uint32_t *)d->scratch.p;
     P.err = (int32_t *)d->err.p;
+    if (!d->task_ctr.p) {
+        const uint32_t zero[2] = {0u, 0u};
+        const int rc = upload(d->task_ctr, zero, 2);
+        if (rc) {
+            delete d;
+            return rc;
+        }
+    }
+    P.task_ctr = (uint32_t *)d->task_ctr.p;
     P.r_f = (const double *)d->r_f.p;
     P.r_g = (const double *)d->r_g.p;
     P.q_bnd = (const double *)d->q_bnd.p;

@@ -23,6 +23,28 @@ struct Op {
     int32_t type, d, node, aux;  // aux: frozen flag for leaves
 };
 
+// Task queue of the persistent decode kernels.
+#ifndef QPD_DYN
+#define QPD_DYN 1  // tasks from a device queue (0: static grid-stride with evened rounds)
+#endif
+
+// One atomic per wave (lane 0, a vector atomic), the old value broadcast.
+__device__ __forceinline__ int64_t wave_take(uint32_t *ctr) {
+    uint32_t v = 0;
+    if (threadIdx.x == 0) v = atomicAdd(ctr, 1u);
+    return (int64_t)__builtin_amdgcn_readfirstlane(v);
+}
+
+// The queue drains only after every wave has taken its last (failed) task;
+// the last wave out zeroes both counters ([0] taken, [1] done) for the next
+// launch.
+__device__ __forceinline__ void queue_done(uint32_t *ctr) {
+    if (QPD_DYN && wave_take(ctr + 1) == gridDim.x - 1 && threadIdx.x == 0) {
+        atomicExch(ctr, 0u);
+        atomicExch(ctr + 1, 0u);
+    }
+}
+
 constexpr int kMaxDepth = 16;  // N <= 65536
 constexpr int kMaxL = 8;       // fast engine: 2L <= 16, libstdc++ sorts by insertion (stable)
 constexpr int kMaxM = kMaxL - 1;

@@ -99,17 +99,6 @@ struct FastPlan {
 #define QPD_EXP_SLABMUL 1
 #endif
 
-#ifndef QPD_DYN
-#define QPD_DYN 1  // tasks from a device queue (0: static grid-stride with evened rounds)
-#endif
-
-// One atomic per wave (lane 0, a vector atomic), the old value broadcast.
-__device__ __forceinline__ int64_t wave_take(uint32_t *ctr) {
-    uint32_t v = 0;
-    if (threadIdx.x == 0) v = atomicAdd(ctr, 1u);
-    return (int64_t)__builtin_amdgcn_readfirstlane(v);
-}
-
 #ifndef QPD_SLAB_AUX
 #define QPD_SLAB_AUX 0  // cache-policy bits of the slab's buffer ops (2 = nt)
 #endif
@@ -1490,12 +1479,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
         }
 #endif
     }
-    // The queue drains only after every wave has taken its last (failed)
-    // task; the last wave out zeroes both counters for the next launch.
-    if (QPD_DYN && wave_take(P.task_ctr + 1) == gridDim.x - 1 && threadIdx.x == 0) {
-        atomicExch(P.task_ctr, 0u);
-        atomicExch(P.task_ctr + 1, 0u);
-    }
+    queue_done(P.task_ctr);
 }
 
 // ---------------------------------------------------------------------------

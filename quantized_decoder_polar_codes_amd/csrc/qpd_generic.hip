@@ -72,6 +72,7 @@ struct DevPlan {
     const int32_t *info_pos;
     uint32_t *scratch;
     int32_t *err;
+    uint32_t *task_ctr;  // task queue ([0] taken, [1] waves done; 0 between launches)
 };
 
 __device__ __forceinline__ double vcl_at(const DevPlan &P, int row, int pos, int sym) {
@@ -355,7 +356,9 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
     PT self = 0;
     for (int d = 0; d <= kMaxDepth && PtrW<ML>::B * (d + 1) <= (int)(8 * sizeof(PT)); ++d) self = gp_set<ML>(self, d, gl);
 
-    for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    // groups: the first blockIdx.x, then the next untaken one (qpd_common.hpp)
+    for (int64_t grp = blockIdx.x; grp < ngroups;
+         grp = QPD_DYN ? (int64_t)gridDim.x + wave_take(P.task_ctr) : grp + gridDim.x) {
         int64_t frame = grp * P.fpw + lane / gs;
         const bool frame_ok = frame < B;
         if (!frame_ok) frame = B - 1;
@@ -708,6 +711,7 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
         }
         wave_sync();
     }
+    queue_done(P.task_ctr);
 }
 
 }  // namespace qpd
