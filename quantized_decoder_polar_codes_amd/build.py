@@ -24,30 +24,38 @@ def needs_build() -> bool:
     return any(os.path.getmtime(s) > t for s in _sources())
 
 
+# Translation units and their own flags.  The FastSCL-LUT kernels take the
+# max-ILP machine scheduler (measured +5 % there, -0.5 % on SCL-LUT; see
+# qpd_fast_fscl.hip), so they are a separate unit.
+UNITS = [
+    ("qpd_capi.hip", []),
+    ("qpd_fast_fscl.hip", ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]),
+    ("qpd_lutgen.cpp", []),
+]
+
+
 def build_native(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return LIB
-    cmd = [
-        HIPCC,
-        f"--offload-arch={ARCH}",
-        "-O3",
-        "-std=c++17",
-        "-fPIC",
-        "-shared",
-        "-Wall",
-        "-Wno-unused-function",
-        "-I",
-        os.path.join(ROOT, "include"),
-        "-I",
-        SRC,
-        os.path.join(SRC, "qpd_capi.hip"),
-        os.path.join(SRC, "qpd_lutgen.cpp"),
-        "-o",
-        LIB + ".tmp",
-    ]
+    common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+              "-I", os.path.join(ROOT, "include"), "-I", SRC]
+    objs, procs = [], []
+    for src, extra in UNITS:  # the units compile in parallel
+        obj = os.path.join(HERE, os.path.splitext(src)[0] + ".o")
+        cmd = common + extra + ["-c", os.path.join(SRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        objs.append(obj)
+        procs.append((cmd, subprocess.Popen(cmd)))
+    for cmd, p in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, cmd)
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", LIB + ".tmp"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
+    for o in objs:
+        os.remove(o)
     os.replace(LIB + ".tmp", LIB)
     return LIB
 

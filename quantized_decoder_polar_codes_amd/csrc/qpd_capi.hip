@@ -13,6 +13,10 @@
 #include "qpd.h"
 #include "qpd_generic.hip"
 #include "qpd_fast.hip"
+
+namespace qpd {
+const void *fast_kernel_fscl(int sets, bool l8, bool r1l);  // qpd_fast_fscl.hip
+}
 #include "qpd_mc.hip"
 #include "qpd_probe.hip"
 
@@ -524,12 +528,16 @@ const void *fast_kernel(int kind, int sets, bool l8, bool r1l) {
             if (sets == 2) return l8 ? QPD_FK(K_SCL_LUT, 2, true) : QPD_FK(K_SCL_LUT, 2, false);
             return l8 ? QPD_FK(K_SCL_LUT, 1, true) : QPD_FK(K_SCL_LUT, 1, false);
         case QPD_FASTSCL_LUT:
+#ifndef QPD_STAMPS
+            return fast_kernel_fscl(sets, l8, r1l);  // qpd_fast_fscl.hip (own scheduler flags)
+#else
             if (r1l) {
                 if (sets == 2) return l8 ? QPD_FKR(2, true) : QPD_FKR(2, false);
                 return l8 ? QPD_FKR(1, true) : QPD_FKR(1, false);
             }
             if (sets == 2) return l8 ? QPD_FK(K_FASTSCL_LUT, 2, true) : QPD_FK(K_FASTSCL_LUT, 2, false);
             return l8 ? QPD_FK(K_FASTSCL_LUT, 1, true) : QPD_FK(K_FASTSCL_LUT, 1, false);
+#endif
         default: return nullptr;
     }
 #undef QPD_FKR

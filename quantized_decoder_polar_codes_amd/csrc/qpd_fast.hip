@@ -1171,6 +1171,16 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
     // or the grid-stride successor.
     for (int64_t task = blockIdx.x; task < ntasks;
          task = QPD_DYN ? (int64_t)gridDim.x + wave_take(P.task_ctr) : task + gridDim.x) {
+#ifdef QPD_POISON
+        // Diagnosis builds only: every LDS word and slab row of this wave set to
+        // QPD_POISON at the start of each task, so that a read of a row no op of
+        // this task wrote shows up as a parity difference.
+        for (int i = threadIdx.x; i < NS * sstride; i += 64) lds_dyn[i] = (uint32_t)QPD_POISON;
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+            for (int r = 0; r < P.glb_rows; ++r) Mv[s].gp[r * 64 + threadIdx.x] = (uint32_t)QPD_POISON;
+        wave_sync();
+#endif
         Path stv[NS];
         {
             const int lane = threadIdx.x, gl = lane & (gs - 1);
@@ -1482,6 +1492,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
     queue_done(P.task_ctr);
 }
 
+#ifndef QPD_FAST_TEMPLATES_ONLY  // qpd_fast_fscl.hip: the decode kernel templates only
 // ---------------------------------------------------------------------------
 // Root pre-pass (pre-mode: N >= 16, the root's left child a plain node).
 // The root's f and both g variants depend on the channel symbols only, yet
@@ -1522,5 +1533,6 @@ __global__ __launch_bounds__(256) void root_pre_kernel(FastPlan P, const int32_t
         }
     }
 }
+#endif  // QPD_FAST_TEMPLATES_ONLY
 
 }  // namespace qpd
