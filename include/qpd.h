@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define QPD_ABI_VERSION 3
+#define QPD_ABI_VERSION 4
 
 /* Decoder kinds (the reference's class names). */
 enum qpd_kind {
@@ -167,16 +167,25 @@ enum qpd_engine { QPD_ENGINE_AUTO = 0, QPD_ENGINE_GENERIC = 1, QPD_ENGINE_FAST =
 typedef struct qpd_decoder qpd_decoder;
 
 int qpd_abi_version(void);
+/* Hash of the sources and flags the library was built from (build.py
+ * source_hash): the Python loader refuses a library built from other sources. */
+const char *qpd_build_id(void);
 const char *qpd_last_error(void);
 
 int qpd_create(const qpd_config *cfg, qpd_decoder **out);
 void qpd_destroy(qpd_decoder *dec);
 
 /* LUT kinds.  d_symbols: device int32 [B][N]; d_out: device uint8 [B][K]
- * ([B][A] for the CRC-aided kinds; qpd_info.out_bits).
- * A decoder owns its work buffers (slab, pre-pass rows, task queue): calls on
- * one decoder must be ordered (one stream at a time); use one decoder per
- * concurrent stream. */
+ * ([B][A] for the CRC-aided kinds; qpd_info.out_bits).  Asynchronous on
+ * `stream`.
+ * A decoder owns its work buffers (slab, pre-pass rows, task queue, error
+ * word, staging), so the library orders its calls: a call on a stream other
+ * than the one the decoder's previous work ran on first makes that stream wait
+ * for it (hipStreamWaitEvent), and host threads are serialized per handle.
+ * Any mix of streams and host threads on one decoder therefore decodes as if
+ * the calls ran one after another (the reference's synchronous contract,
+ * py_SCLLUTDecoder.cpp:15); concurrent streams on ONE decoder do not overlap
+ * -- use one decoder per stream for that. */
 int qpd_decode(qpd_decoder *dec, const int32_t *d_symbols, int64_t B, uint8_t *d_out, void *stream);
 /* float64-LLR kinds (QPD_SC_FLOAT, 7..14).  d_llr: device float64 [B][N];
  * d_out: device uint8 [B][K] ([B][A] for QPD_CASCL_FLOAT). */
@@ -189,7 +198,8 @@ int qpd_decode_f64_host(qpd_decoder *dec, const double *h_llr, int64_t B, uint8_
 /* Returns QPD_E_INPUT (and clears the flags) if any decode since the last
  * check saw a channel symbol outside [0, v), a Lloyd bisect index outside
  * the reconstruction list, or a NaN path metric reaching a list selection
- * (each undefined behaviour in the reference); synchronizes the device. */
+ * (each undefined behaviour in the reference); waits for the decoder's
+ * previous work (not the whole device). */
 int qpd_check_input_error(qpd_decoder *dec);
 
 /*

@@ -17,13 +17,14 @@ LIB_PATH = os.environ.get("QPD_LIB") or os.path.join(HERE, "libqpd.so")
  QPD_SCL_LLOYD) = range(15)
 FLOAT_KINDS = (QPD_SC_FLOAT, QPD_SCL_FLOAT, QPD_CASCL_FLOAT, QPD_FASTSC_FLOAT, QPD_FASTSCL_FLOAT, QPD_SC_UNIFORM,
                QPD_SCL_UNIFORM, QPD_SC_LLOYD, QPD_SCL_LLOYD)
-ABI_VERSION = 3
+ABI_VERSION = 4
 QPD_ENGINE_AUTO, QPD_ENGINE_GENERIC, QPD_ENGINE_FAST = range(3)
 QPD_OK, QPD_E_INVALID, QPD_E_UNSUPPORTED, QPD_E_DEVICE, QPD_E_INPUT = 0, -1, -2, -3, -4
 
 # Every symbol include/qpd.h declares (tests check the library exports them).
 EXPORTED = (
     "qpd_abi_version",
+    "qpd_build_id",
     "qpd_last_error",
     "qpd_create",
     "qpd_destroy",
@@ -175,8 +176,26 @@ def load():
     L.qpd_probe_lds.restype = ctypes.c_int
     if L.qpd_abi_version() != ABI_VERSION:
         raise ImportError("libqpd.so ABI version mismatch")
+    L.qpd_build_id.restype = ctypes.c_char_p
+    check_build_id(L)
     _lib = L
     return L
+
+
+def check_build_id(L) -> None:
+    """The in-tree library must be built from the sources next to it (build.py
+    stamps their hash into it): a stale binary raises instead of running.
+    QPD_LIB (an explicitly chosen diagnostic build) skips the check."""
+    if os.environ.get("QPD_LIB"):
+        return
+    from . import build
+
+    if not os.path.isdir(build.SRC):  # a library shipped without its sources
+        return
+    have, want = L.qpd_build_id().decode(), build.source_hash()
+    if have != want:
+        raise ImportError(f"{LIB_PATH} was built from other sources (build id {have}, tree {want}): rebuild it "
+                          "with `python -c 'import __graft_entry__ as g; g.build()'`")
 
 
 def check(rc: int) -> None:

@@ -2,6 +2,7 @@
 the .so lands next to this file so it travels to the GPU box with the repo."""
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 
@@ -17,13 +18,6 @@ def _sources():
     return [os.path.join(SRC, f) for f in sorted(os.listdir(SRC))] + [os.path.join(ROOT, "include", "qpd.h")]
 
 
-def needs_build() -> bool:
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(s) > t for s in _sources())
-
-
 # Translation units and their own flags.  The FastSCL-LUT kernels take the
 # max-ILP machine scheduler (measured +5 % there, -0.5 % on SCL-LUT; see
 # qpd_fast_fscl.hip), so they are a separate unit.
@@ -32,13 +26,49 @@ UNITS = [
     ("qpd_fast_fscl.hip", ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]),
     ("qpd_lutgen.cpp", []),
 ]
+COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
+
+
+def source_hash() -> str:
+    """SHA-256 over every source file, the target and the compile flags: the
+    build id stamped into libqpd.so (qpd_build_id) and checked when the
+    library is loaded, so a shipped binary provably matches the tree."""
+    h = hashlib.sha256()
+    h.update(repr((ARCH, COMMON_FLAGS, UNITS)).encode())
+    for path in _sources():
+        h.update(os.path.relpath(path, ROOT).encode() + b"\0")
+        with open(path, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()[:32]
+
+
+BUILD_ID_TAG = b"qpd-build-id:"
+
+
+def library_build_id(path: str = LIB) -> str | None:
+    """The build id embedded in a built library (read from its bytes, no dlopen)."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    i = data.find(BUILD_ID_TAG)
+    if i < 0:
+        return None
+    return data[i + len(BUILD_ID_TAG): i + len(BUILD_ID_TAG) + 32].decode("ascii", "replace")
+
+
+def needs_build() -> bool:
+    return library_build_id() != source_hash()
 
 
 def build_native(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return LIB
-    common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-              "-I", os.path.join(ROOT, "include"), "-I", SRC]
+    bid = source_hash()
+    common = [HIPCC, f"--offload-arch={ARCH}"] + COMMON_FLAGS + ["-I", os.path.join(ROOT, "include"), "-I", SRC,
+                                                                 f'-DQPD_BUILD_ID="{bid}"']
     objs, procs = [], []
     for src, extra in UNITS:  # the units compile in parallel
         obj = os.path.join(HERE, os.path.splitext(src)[0] + ".o")

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -132,15 +133,31 @@ struct qpd_decoder {
     // staging for the host-buffer entry points
     DeviceBuf h_in, h_out;
     size_t h_in_bytes = 0, h_out_bytes = 0;
-    // host-buffer entry points: own stream and a pinned staging buffer (one
-    // stream synchronization per call: copy in, decode, copy out + error word)
+    // The decoder's own stream (created with the handle): every upload of
+    // qpd_create, the host-buffer entry points (pinned staging, one stream
+    // synchronization per call: copy in, decode, copy out + error word) and
+    // the error-word checks run on it.
     hipStream_t hs = nullptr;
     void *pin = nullptr;
     size_t pin_bytes = 0;
+    // Ordering across streams (thread-safe per handle per
+    // stream).  The work buffers (slab, pre-pass rows, task queue, error word,
+    // staging) are per decoder, so every call first makes its stream wait for
+    // the decoder's previous work when that ran on another stream
+    // (hipStreamWaitEvent on `last_ev`), and records `last_ev` on its own
+    // stream after its launches.  `mu` serializes host threads on one handle.
+    std::mutex mu;
+    hipEvent_t last_ev = nullptr;
+    hipStream_t last_st = nullptr;
+    bool last_valid = false;
+    uint32_t task_base = 0;  // task queue counter at the start of the next launch (wave_take)
     // qpd_profile: HIP events around every launch, per kernel class
     bool prof = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[QPD_KC_COUNT];
     ~qpd_decoder() {
+        if (last_valid) (void)hipEventSynchronize(last_ev);  // no buffer is freed under a running launch
+        if (hs) (void)hipStreamSynchronize(hs);
+        if (last_ev) (void)hipEventDestroy(last_ev);
         if (hs) (void)hipStreamDestroy(hs);
         if (pin) (void)hipHostFree(pin);
         for (auto &v : prof_ev)
@@ -153,11 +170,17 @@ struct qpd_decoder {
 
 namespace {
 
+// Device copy of a host array on the decoder's own stream, complete on return
+// (qpd_create: every table is resident before the handle is handed out, so no
+// decode on any stream can overtake an upload).
 template <class T>
-int upload(DeviceBuf &b, const T *src, size_t count) {
+int upload(DeviceBuf &b, const T *src, size_t count, hipStream_t st) {
     const size_t bytes = std::max<size_t>(1, count * sizeof(T));
     QPD_HIP(hipMalloc(&b.p, bytes));
-    if (count) QPD_HIP(hipMemcpy(b.p, src, count * sizeof(T), hipMemcpyHostToDevice));
+    if (count) {
+        QPD_HIP(hipMemcpyAsync(b.p, src, count * sizeof(T), hipMemcpyHostToDevice, st));
+        QPD_HIP(hipStreamSynchronize(st));
+    }
     return QPD_OK;
 }
 
@@ -166,19 +189,47 @@ int set_device(const qpd_decoder *d) {
     return QPD_OK;
 }
 
+// Cross-stream ordering of one decoder's work (see qpd_decoder::last_ev):
+// `order_on` before a call's first operation on stream st, `mark_on` after
+// its last.
+int order_on(qpd_decoder *d, hipStream_t st) {
+    if (d->last_valid && d->last_st != st) QPD_HIP(hipStreamWaitEvent(st, d->last_ev, 0));
+    return QPD_OK;
+}
+
+int mark_on(qpd_decoder *d, hipStream_t st) {
+    if (!d->last_ev) QPD_HIP(hipEventCreateWithFlags(&d->last_ev, hipEventDisableTiming));
+    QPD_HIP(hipEventRecord(d->last_ev, st));
+    d->last_st = st;
+    d->last_valid = true;
+    return QPD_OK;
+}
+
 // One kernel launch of class kc on stream st; bracketed by HIP events on that
 // stream while profiling is enabled (qpd_profile / qpd_kernel_times).
 template <class F>
 int timed_launch(qpd_decoder *d, int kc, hipStream_t st, F &&launch) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    auto drop = [&]() {  // no event outlives a failed record or launch
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+    };
     if (d->prof) {
-        QPD_HIP(hipEventCreate(&e0));
-        QPD_HIP(hipEventCreate(&e1));
-        QPD_HIP(hipEventRecord(e0, st));
+        hipError_t e = hipEventCreate(&e0);
+        if (e == hipSuccess) e = hipEventCreate(&e1);
+        if (e == hipSuccess) e = hipEventRecord(e0, st);
+        if (e != hipSuccess) {
+            drop();
+            return fail(QPD_E_DEVICE, std::string("profiling event: ") + hipGetErrorString(e));
+        }
     }
     const int rc = launch();
     if (d->prof) {
-        QPD_HIP(hipEventRecord(e1, st));
+        const hipError_t e = rc ? hipSuccess : hipEventRecord(e1, st);
+        if (rc || e != hipSuccess) {
+            drop();
+            return rc ? rc : fail(QPD_E_DEVICE, std::string("profiling event: ") + hipGetErrorString(e));
+        }
         d->prof_ev[kc].emplace_back(e0, e1);
     }
     return rc;
@@ -544,6 +595,19 @@ const void *fast_kernel(int kind, int sets, bool l8, bool r1l) {
 #undef QPD_FK
 }
 
+// Task queue of the persistent kernels: one counter, never reset (wave_take).
+// QPD_TASK_BASE0 (tests only) starts it elsewhere, e.g. just below 2^32 so
+// that the first launches wrap around.
+int init_task_queue(qpd_decoder *d) {
+    uint32_t v0 = 0;
+    if (const char *e = getenv("QPD_TASK_BASE0")) v0 = (uint32_t)strtoull(e, nullptr, 0);
+    const uint32_t init[2] = {v0, 0u};
+    const int rc = upload(d->task_ctr, init, 2, d->hs);
+    if (rc) return rc;
+    d->task_base = v0;
+    return QPD_OK;
+}
+
 int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     qpd::FastPlan &F = d->fplan;
     const int N = c->N, n = d->n, v = c->v;
@@ -670,7 +734,7 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     fast_ops(mops, Ly, c->kind, N, n, v, c->frozen_bits, nt_fast, c->vcl, r1tab, 0, 0);
     if (r1tab.empty()) r1tab.push_back(0);
     {
-        int rc = upload(d->r1_rank, r1tab.data(), r1tab.size());
+        int rc = upload(d->r1_rank, r1tab.data(), r1tab.size(), d->hs);
         if (rc) return rc;
     }
     F.r1_rank = (const uint16_t *)d->r1_rank.p;
@@ -681,7 +745,7 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     F.nops = (int)mops.size();
     d->num_mops = F.nops;
     {
-        int rc = upload(d->mops, mops.data(), mops.size());
+        int rc = upload(d->mops, mops.data(), mops.size(), d->hs);
         if (rc) return rc;
     }
     // nibble-packed tables: entry (u, a, b) of node p at bit 4*(idx&7) of dword idx>>3
@@ -700,9 +764,9 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
                 }
             }
     }
-    int rc = upload(d->f_tab, ft.data(), ft.size());
+    int rc = upload(d->f_tab, ft.data(), ft.size(), d->hs);
     if (rc) return rc;
-    rc = upload(d->g_tab, gt.data(), gt.size());
+    rc = upload(d->g_tab, gt.data(), gt.size(), d->hs);
     if (rc) return rc;
     const int64_t per_wave = (int64_t)NS * F.glb_rows * 64 * 4;
     // Persistent grid: as many waves as can be resident at once.
@@ -727,11 +791,8 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     F.info_pos = (const int32_t *)d->info_pos.p;
     F.scratch = (uint32_t *)d->fscratch.p;
     F.err = (int32_t *)d->err.p;
-    {
-        const uint32_t zero[2] = {0u, 0u};  // task queue: [0] tasks taken, [1] waves done
-        rc = upload(d->task_ctr, zero, 2);
-        if (rc) return rc;
-    }
+    rc = init_task_queue(d);
+    if (rc) return rc;
     F.task_ctr = (uint32_t *)d->task_ctr.p;
     return QPD_OK;
 }
@@ -779,13 +840,16 @@ int launch_generic(qpd_decoder *d, const In *in, int64_t B, uint8_t *out, int gr
     const void *kfn = generic_kernel(d->kind, d->dom, d->L > qpd::kMaxL);
     if (!kfn) return fail(QPD_E_INVALID, "bad kind");
     qpd::DevPlan P = d->plan;
+    P.task_base = d->task_base;
     const In *in_arg = in;
     void *args[] = {&P, &in_arg, &B, &out};
-    return timed_launch(d, QPD_KC_DECODE, st, [&]() -> int {
+    const int rc = timed_launch(d, QPD_KC_DECODE, st, [&]() -> int {
         QPD_HIP(hipLaunchKernel(kfn, dim3(grid), dim3(64), args, 0, st));
         QPD_HIP(hipGetLastError());
         return QPD_OK;
     });
+    if (!rc) d->task_base += (uint32_t)((B + d->plan.fpw - 1) / d->plan.fpw);  // takes of this launch (wave_take)
+    return rc;
 }
 
 }  // namespace
@@ -793,6 +857,15 @@ int launch_generic(qpd_decoder *d, const In *in, int64_t B, uint8_t *out, int gr
 extern "C" {
 
 int qpd_abi_version(void) { return QPD_ABI_VERSION; }
+
+// Source hash of the tree this library was built from (build.py:
+// source_hash); the tagged string is also found in the file's bytes.
+#ifndef QPD_BUILD_ID
+#define QPD_BUILD_ID "unstamped-build"
+#endif
+__attribute__((used)) static const char kBuildIdTag[] = "qpd-build-id:" QPD_BUILD_ID;
+
+const char *qpd_build_id(void) { return kBuildIdTag + sizeof("qpd-build-id:") - 1; }
 
 const char *qpd_last_error(void) { return g_err.c_str(); }
 
@@ -811,6 +884,13 @@ int qpd_create(const qpd_config *cfg, qpd_decoder **out) {
     if (c->device >= 0) QPD_HIP(hipSetDevice(c->device));
 
     qpd_decoder *d = new qpd_decoder();
+    {
+        const hipError_t e = hipStreamCreateWithFlags(&d->hs, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            delete d;
+            return fail(QPD_E_DEVICE, std::string("decoder stream: ") + hipGetErrorString(e));
+        }
+    }
     d->pub_kind = cfg->kind;
     d->dom = dom;
     d->out_bits = ca ? cfg->A : cfg->K;
@@ -903,31 +983,31 @@ int qpd_create(const qpd_config *cfg, qpd_decoder **out) {
             return rc_;       \
         }                     \
     } while (0)
-    QPD_TRY(upload(d->ops, s.ops.data(), s.ops.size()));
-    QPD_TRY(upload(d->info_pos, info.data(), info.size()));
+    QPD_TRY(upload(d->ops, s.ops.data(), s.ops.size(), d->hs));
+    QPD_TRY(upload(d->info_pos, info.data(), info.size(), d->hs));
     {
         std::vector<uint32_t> mask((N + 31) / 32, 0u);
         for (int i : info) mask[i >> 5] |= 1u << (i & 31);
-        QPD_TRY(upload(d->info_mask, mask.data(), mask.size()));
+        QPD_TRY(upload(d->info_mask, mask.data(), mask.size(), d->hs));
     }
     if (dom == qpd::DOM_UNIFORM) {
-        QPD_TRY(upload(d->r_f, c->r_f, (size_t)N - 1));
-        QPD_TRY(upload(d->r_g, c->r_g, (size_t)N - 1));
+        QPD_TRY(upload(d->r_f, c->r_f, (size_t)N - 1, d->hs));
+        QPD_TRY(upload(d->r_g, c->r_g, (size_t)N - 1, d->hs));
     } else if (dom == qpd::DOM_LLOYD) {
-        QPD_TRY(upload(d->q_bnd, c->q_bnd, (size_t)c->q_bnd_count));
-        QPD_TRY(upload(d->q_rec, c->q_rec, (size_t)c->q_rec_count));
-        QPD_TRY(upload(d->bnd_off, c->bnd_off, 2 * ((size_t)N - 1)));
-        QPD_TRY(upload(d->bnd_len, c->bnd_len, 2 * ((size_t)N - 1)));
-        QPD_TRY(upload(d->rec_off, c->rec_off, 2 * ((size_t)N - 1)));
-        QPD_TRY(upload(d->rec_len, c->rec_len, 2 * ((size_t)N - 1)));
+        QPD_TRY(upload(d->q_bnd, c->q_bnd, (size_t)c->q_bnd_count, d->hs));
+        QPD_TRY(upload(d->q_rec, c->q_rec, (size_t)c->q_rec_count, d->hs));
+        QPD_TRY(upload(d->bnd_off, c->bnd_off, 2 * ((size_t)N - 1), d->hs));
+        QPD_TRY(upload(d->bnd_len, c->bnd_len, 2 * ((size_t)N - 1), d->hs));
+        QPD_TRY(upload(d->rec_off, c->rec_off, 2 * ((size_t)N - 1), d->hs));
+        QPD_TRY(upload(d->rec_len, c->rec_len, 2 * ((size_t)N - 1), d->hs));
     }
     if (dom == qpd::DOM_LUT) {
         const size_t vv = (size_t)c->v * c->v;
-        QPD_TRY(upload(d->lut_f, c->lut_f, (size_t)c->lut_f_count * vv));
-        QPD_TRY(upload(d->lut_g, c->lut_g, (size_t)c->lut_g_count * 2 * vv));
-        QPD_TRY(upload(d->f_base, c->f_base, (size_t)N - 1));
-        QPD_TRY(upload(d->g_base, c->g_base, (size_t)N - 1));
-        QPD_TRY(upload(d->vcl, c->vcl, (size_t)c->vcl_rows * N * c->v));
+        QPD_TRY(upload(d->lut_f, c->lut_f, (size_t)c->lut_f_count * vv, d->hs));
+        QPD_TRY(upload(d->lut_g, c->lut_g, (size_t)c->lut_g_count * 2 * vv, d->hs));
+        QPD_TRY(upload(d->f_base, c->f_base, (size_t)N - 1, d->hs));
+        QPD_TRY(upload(d->g_base, c->g_base, (size_t)N - 1, d->hs));
+        QPD_TRY(upload(d->vcl, c->vcl, (size_t)c->vcl_rows * N * c->v, d->hs));
     }
     {
         hipError_t e = hipSuccess;
@@ -937,7 +1017,8 @@ int qpd_create(const qpd_config *cfg, qpd_decoder **out) {
             return fail(QPD_E_DEVICE, std::string("scratch hipMalloc: ") + hipGetErrorString(e));
         }
         e = hipMalloc(&d->err.p, sizeof(int32_t));
-        if (e == hipSuccess) e = hipMemset(d->err.p, 0, sizeof(int32_t));
+        if (e == hipSuccess) e = hipMemsetAsync(d->err.p, 0, sizeof(int32_t), d->hs);
+        if (e == hipSuccess) e = hipStreamSynchronize(d->hs);
         if (e != hipSuccess) {
             delete d;
             return fail(QPD_E_DEVICE, std::string("err hipMalloc: ") + hipGetErrorString(e));
@@ -955,8 +1036,7 @@ int qpd_create(const qpd_config *cfg, qpd_decoder **out) {
     P.scratch = (uint32_t *)d->scratch.p;
     P.err = (int32_t *)d->err.p;
     if (!d->task_ctr.p) {
-        const uint32_t zero[2] = {0u, 0u};
-        const int rc = upload(d->task_ctr, zero, 2);
+        const int rc = init_task_queue(d);
         if (rc) {
             delete d;
             return rc;
@@ -991,7 +1071,11 @@ int qpd_create(const qpd_config *cfg, qpd_decoder **out) {
     return QPD_OK;
 }
 
-void qpd_destroy(qpd_decoder *d) { delete d; }
+void qpd_destroy(qpd_decoder *d) {
+    if (!d) return;
+    if (d->device >= 0) (void)hipSetDevice(d->device);
+    delete d;  // ~qpd_decoder waits for the decoder's last work before any buffer is freed
+}
 
 int qpd_get_info(const qpd_decoder *d, qpd_info *info) {
     if (!d || !info) return fail(QPD_E_INVALID, "null argument");
@@ -1012,17 +1096,16 @@ int qpd_get_info(const qpd_decoder *d, qpd_info *info) {
     return QPD_OK;
 }
 
-int qpd_decode(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_out, void *stream) {
-    if (!d) return fail(QPD_E_INVALID, "null decoder");
-    if (d->dom != qpd::DOM_LUT) return fail(QPD_E_INVALID, "this decoder takes float64 LLRs: use qpd_decode_f64");
-    if (B < 0) return fail(QPD_E_INVALID, "negative batch");
-    if (B == 0) return QPD_OK;
-    if (!d_symbols || !d_out) return fail(QPD_E_INVALID, "null buffer");
-    int rc = set_device(d);
-    if (rc) return rc;
+}  // extern "C"
+
+namespace {
+
+// Launches of one device-buffer decode on stream st (caller: lock held,
+// stream ordered).
+int decode_impl(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_out, hipStream_t st) {
+    int rc = QPD_OK;
     const int64_t groups = (B + d->plan.fpw - 1) / d->plan.fpw;
     const int grid = (int)std::min<int64_t>(groups, d->max_waves);
-    hipStream_t st = (hipStream_t)stream;
     if (d->engine == QPD_ENGINE_FAST) {
         const int64_t tw = (int64_t)d->fplan.fpw * d->sets;  // frames per wave task
         const size_t lds = (size_t)d->lds_bytes;
@@ -1039,26 +1122,38 @@ int qpd_decode(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_o
                 fgrid = (int)((fgroups + rounds - 1) / rounds);
             }
             const qpd::MOp *ops_arg = fp.ops;
+            fp.task_base = d->task_base;
             void *args[] = {&fp, &in_arg, &Bc, &out_arg, &ops_arg};
-            return timed_launch(d, QPD_KC_DECODE, st, [&]() -> int {
+            const int lrc = timed_launch(d, QPD_KC_DECODE, st, [&]() -> int {
                 QPD_HIP(hipLaunchKernel(kfn, dim3(fgrid), dim3(64), args, lds, st));
                 QPD_HIP(hipGetLastError());
                 return QPD_OK;
             });
+            if (!lrc) d->task_base += (uint32_t)fgroups;  // takes of this launch (wave_take)
+            return lrc;
         };
         if (!d->pre) {
             fp.in_shift = fp.n;
             return decode(d_symbols, B, d_out);
         }
         // pre-mode: root pre-pass, then the decode on its rows, chunk by chunk
-        const int64_t chunk = std::min<int64_t>(B, d->pre_chunk);
+        int64_t chunk = std::min<int64_t>(B, d->pre_chunk);
         if (d->pre_cap < chunk) {
             if (d->pre_buf.p) QPD_HIP(hipFree(d->pre_buf.p));
             d->pre_buf.p = nullptr;
             d->pre_cap = 0;
-            QPD_HIP(hipMalloc(&d->pre_buf.p, (size_t)chunk * (size_t)fp.N));  // N/4 words per frame
+            // N bytes per frame; on an allocation failure the chunk halves
+            // (fewer frames per decode launch, same results)
+            hipError_t e = hipErrorOutOfMemory;
+            while (chunk >= 1 && (e = hipMalloc(&d->pre_buf.p, (size_t)chunk * (size_t)fp.N)) != hipSuccess) {
+                (void)hipGetLastError();
+                d->pre_buf.p = nullptr;
+                chunk /= 2;
+            }
+            if (e != hipSuccess) return fail(QPD_E_DEVICE, std::string("pre-pass rows hipMalloc: ") + hipGetErrorString(e));
             d->pre_cap = chunk;
         }
+        chunk = std::min<int64_t>(chunk, d->pre_cap);
         uint32_t *pre = (uint32_t *)d->pre_buf.p;
         for (int64_t f0 = 0; f0 < B; f0 += chunk) {
             int64_t Bc = std::min<int64_t>(chunk, B - f0);
@@ -1082,17 +1177,47 @@ int qpd_decode(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_o
     return launch_generic(d, d_symbols, B, d_out, grid, st);
 }
 
+int decode_f64_impl(qpd_decoder *d, const double *d_llr, int64_t B, uint8_t *d_out, hipStream_t st) {
+    const int64_t groups = (B + d->plan.fpw - 1) / d->plan.fpw;
+    const int grid = (int)std::min<int64_t>(groups, d->max_waves);
+    return launch_generic(d, d_llr, B, d_out, grid, st);
+}
+
+// One call's work on stream st, ordered after the decoder's previous work on
+// any other stream, under the handle's lock.
+template <class F>
+int ordered(qpd_decoder *d, hipStream_t st, F &&work) {
+    std::lock_guard<std::mutex> lk(d->mu);
+    int rc = set_device(d);
+    if (rc) return rc;
+    if ((rc = order_on(d, st))) return rc;
+    rc = work();
+    const int mrc = mark_on(d, st);  // also after a failed launch: earlier launches of the call may be queued
+    return rc ? rc : mrc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qpd_decode(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_out, void *stream) {
+    if (!d) return fail(QPD_E_INVALID, "null decoder");
+    if (d->dom != qpd::DOM_LUT) return fail(QPD_E_INVALID, "this decoder takes float64 LLRs: use qpd_decode_f64");
+    if (B < 0) return fail(QPD_E_INVALID, "negative batch");
+    if (B == 0) return QPD_OK;
+    if (!d_symbols || !d_out) return fail(QPD_E_INVALID, "null buffer");
+    hipStream_t st = (hipStream_t)stream;
+    return ordered(d, st, [&]() { return decode_impl(d, d_symbols, B, d_out, st); });
+}
+
 int qpd_decode_f64(qpd_decoder *d, const double *d_llr, int64_t B, uint8_t *d_out, void *stream) {
     if (!d) return fail(QPD_E_INVALID, "null decoder");
     if (d->dom == qpd::DOM_LUT) return fail(QPD_E_INVALID, "LUT decoders take int32 channel symbols: use qpd_decode");
     if (B < 0) return fail(QPD_E_INVALID, "negative batch");
     if (B == 0) return QPD_OK;
     if (!d_llr || !d_out) return fail(QPD_E_INVALID, "null buffer");
-    int rc = set_device(d);
-    if (rc) return rc;
-    const int64_t groups = (B + d->plan.fpw - 1) / d->plan.fpw;
-    const int grid = (int)std::min<int64_t>(groups, d->max_waves);
-    return launch_generic(d, d_llr, B, d_out, grid, (hipStream_t)stream);
+    hipStream_t st = (hipStream_t)stream;
+    return ordered(d, st, [&]() { return decode_f64_impl(d, d_llr, B, d_out, st); });
 }
 
 }  // extern "C"
@@ -1125,69 +1250,75 @@ template <class In, class Dec>
 static int host_roundtrip(qpd_decoder *d, const In *h_in, int64_t B, uint8_t *h_out, Dec dec) {
     const size_t in_b = (size_t)B * d->N * sizeof(In), out_b = (size_t)B * d->out_bits;
     const size_t out_at = (in_b + 15) & ~(size_t)15, err_at = out_at + ((out_b + 15) & ~(size_t)15);
-    int rc = ensure(d->h_in, d->h_in_bytes, in_b);
-    if (rc) return rc;
-    if ((rc = ensure(d->h_out, d->h_out_bytes, std::max<size_t>(1, out_b)))) return rc;
-    if (!d->hs) QPD_HIP(hipStreamCreateWithFlags(&d->hs, hipStreamNonBlocking));
-    if (d->pin_bytes < err_at + 16) {
-        if (d->pin) QPD_HIP(hipHostFree(d->pin));
-        d->pin = nullptr;
-        d->pin_bytes = 0;
-        QPD_HIP(hipHostMalloc(&d->pin, err_at + 16, hipHostMallocDefault));
-        d->pin_bytes = err_at + 16;
-    }
-    char *pin = (char *)d->pin;
-    std::memcpy(pin, h_in, in_b);
-    QPD_HIP(hipMemcpyAsync(d->h_in.p, pin, in_b, hipMemcpyHostToDevice, d->hs));
-    if ((rc = dec((const In *)d->h_in.p, (uint8_t *)d->h_out.p, d->hs))) return rc;
-    if (out_b) QPD_HIP(hipMemcpyAsync(pin + out_at, d->h_out.p, out_b, hipMemcpyDeviceToHost, d->hs));
-    QPD_HIP(hipMemcpyAsync(pin + err_at, d->err.p, sizeof(int32_t), hipMemcpyDeviceToHost, d->hs));
-    QPD_HIP(hipStreamSynchronize(d->hs));
-    std::memcpy(h_out, pin + out_at, out_b);
-    int32_t flag = 0;
-    std::memcpy(&flag, pin + err_at, sizeof(flag));
-    if (flag) {
-        QPD_HIP(hipMemsetAsync(d->err.p, 0, sizeof(int32_t), d->hs));
-        QPD_HIP(hipStreamSynchronize(d->hs));
-        return input_error(flag);
-    }
-    return QPD_OK;
+    hipStream_t hs = d->hs;
+    return ordered(d, hs, [&]() -> int {
+        // the staging buffers may still be read by the previous call's work
+        // only if that ran on hs, which the synchronization below has drained
+        int rc = ensure(d->h_in, d->h_in_bytes, in_b);
+        if (rc) return rc;
+        if ((rc = ensure(d->h_out, d->h_out_bytes, std::max<size_t>(1, out_b)))) return rc;
+        if (d->pin_bytes < err_at + 16) {
+            if (d->pin) QPD_HIP(hipHostFree(d->pin));
+            d->pin = nullptr;
+            d->pin_bytes = 0;
+            QPD_HIP(hipHostMalloc(&d->pin, err_at + 16, hipHostMallocDefault));
+            d->pin_bytes = err_at + 16;
+        }
+        char *pin = (char *)d->pin;
+        std::memcpy(pin, h_in, in_b);
+        QPD_HIP(hipMemcpyAsync(d->h_in.p, pin, in_b, hipMemcpyHostToDevice, hs));
+        if ((rc = dec((const In *)d->h_in.p, (uint8_t *)d->h_out.p, hs))) return rc;
+        if (out_b) QPD_HIP(hipMemcpyAsync(pin + out_at, d->h_out.p, out_b, hipMemcpyDeviceToHost, hs));
+        QPD_HIP(hipMemcpyAsync(pin + err_at, d->err.p, sizeof(int32_t), hipMemcpyDeviceToHost, hs));
+        QPD_HIP(hipStreamSynchronize(hs));
+        std::memcpy(h_out, pin + out_at, out_b);
+        int32_t flag = 0;
+        std::memcpy(&flag, pin + err_at, sizeof(flag));
+        if (flag) {
+            QPD_HIP(hipMemsetAsync(d->err.p, 0, sizeof(int32_t), hs));
+            QPD_HIP(hipStreamSynchronize(hs));
+            return input_error(flag);
+        }
+        return QPD_OK;
+    });
 }
 
 extern "C" {
 
 int qpd_check_input_error(qpd_decoder *d) {
     if (!d) return fail(QPD_E_INVALID, "null decoder");
-    int rc = set_device(d);
-    if (rc) return rc;
-    int32_t flag = 0;
-    QPD_HIP(hipDeviceSynchronize());
-    QPD_HIP(hipMemcpy(&flag, d->err.p, sizeof(flag), hipMemcpyDeviceToHost));
-    if (flag) {
-        QPD_HIP(hipMemset(d->err.p, 0, sizeof(int32_t)));
-        return input_error(flag);
-    }
-    return QPD_OK;
+    hipStream_t hs = d->hs;
+    return ordered(d, hs, [&]() -> int {
+        // hs waits for the decoder's last launch (any stream); the flag is
+        // read and cleared on hs, which later calls on other streams wait for
+        int32_t flag = 0;
+        QPD_HIP(hipMemcpyAsync(&flag, d->err.p, sizeof(flag), hipMemcpyDeviceToHost, hs));
+        QPD_HIP(hipStreamSynchronize(hs));
+        if (flag) {
+            QPD_HIP(hipMemsetAsync(d->err.p, 0, sizeof(int32_t), hs));
+            QPD_HIP(hipStreamSynchronize(hs));
+            return input_error(flag);
+        }
+        return QPD_OK;
+    });
 }
 
 int qpd_decode_host(qpd_decoder *d, const int32_t *h_symbols, int64_t B, uint8_t *h_out) {
     if (!d) return fail(QPD_E_INVALID, "null decoder");
+    if (d->dom != qpd::DOM_LUT) return fail(QPD_E_INVALID, "this decoder takes float64 LLRs: use qpd_decode_f64_host");
     if (B <= 0) return B == 0 ? QPD_OK : fail(QPD_E_INVALID, "negative batch");
     if (!h_symbols || !h_out) return fail(QPD_E_INVALID, "null buffer");
-    int rc = set_device(d);
-    if (rc) return rc;
     return host_roundtrip(d, h_symbols, B, h_out,
-                          [&](const int32_t *in, uint8_t *out, hipStream_t st) { return qpd_decode(d, in, B, out, st); });
+                          [&](const int32_t *in, uint8_t *out, hipStream_t st) { return decode_impl(d, in, B, out, st); });
 }
 
 int qpd_decode_f64_host(qpd_decoder *d, const double *h_llr, int64_t B, uint8_t *h_out) {
     if (!d) return fail(QPD_E_INVALID, "null decoder");
+    if (d->dom == qpd::DOM_LUT) return fail(QPD_E_INVALID, "LUT decoders take int32 channel symbols: use qpd_decode_host");
     if (B <= 0) return B == 0 ? QPD_OK : fail(QPD_E_INVALID, "negative batch");
     if (!h_llr || !h_out) return fail(QPD_E_INVALID, "null buffer");
-    int rc = set_device(d);
-    if (rc) return rc;
     return host_roundtrip(d, h_llr, B, h_out,
-                          [&](const double *in, uint8_t *out, hipStream_t st) { return qpd_decode_f64(d, in, B, out, st); });
+                          [&](const double *in, uint8_t *out, hipStream_t st) { return decode_f64_impl(d, in, B, out, st); });
 }
 
 int qpd_mc_frames(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64_t frame0, int64_t B, uint8_t *d_msg,
@@ -1203,59 +1334,60 @@ int qpd_mc_frames(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64
         if (!(ch->edges[i] <= ch->edges[i + 1])) return fail(QPD_E_INVALID, "edges must be ascending");
         if (ch->lut[i] < 0 || ch->lut[i] >= ch->q) return fail(QPD_E_INVALID, "lut entry outside [0, q)");
     }
-    int rc = set_device(d);
-    if (rc) return rc;
-    if (!d->mc_pref.p) {  // per-decoder constants of the generator, built at the first call
-        const int nw = (d->N + 31) / 32;
-        std::vector<int32_t> pref(nw, 0);
-        std::vector<uint32_t> mask(nw, 0u);
-        QPD_HIP(hipMemcpy(mask.data(), d->info_mask.p, nw * sizeof(uint32_t), hipMemcpyDeviceToHost));
-        for (int w = 1; w < nw; ++w) pref[w] = pref[w - 1] + __builtin_popcount(mask[w - 1]);
-        // CRC register after message bit j and A-1-j zero bits (the register is
-        // linear in the message bits, utils.cpp:77-92): tab[A-1] = taps,
-        // tab[j] = one zero step of tab[j+1]
-        const int A = d->crc_n > 0 ? d->ca_A : 0;
-        std::vector<uint32_t> tab(std::max(A, 1), 0u);
-        if (A > 0) {
-            const uint32_t top = 1u << (d->crc_n - 1), msk = (top << 1) - 1u;
-            tab[A - 1] = d->crc_q & msk;
-            for (int j = A - 2; j >= 0; --j) {
-                const uint32_t r = tab[j + 1];
-                tab[j] = ((r << 1) & msk) ^ ((r & top) ? d->crc_q : 0u);
+    hipStream_t st = (hipStream_t)stream;
+    return ordered(d, st, [&]() -> int {
+        if (!d->mc_pref.p) {  // per-decoder constants of the generator, built at the first call
+            const int nw = (d->N + 31) / 32;
+            std::vector<int32_t> pref(nw, 0);
+            std::vector<uint32_t> mask(nw, 0u);
+            QPD_HIP(hipMemcpyAsync(mask.data(), d->info_mask.p, nw * sizeof(uint32_t), hipMemcpyDeviceToHost, d->hs));
+            QPD_HIP(hipStreamSynchronize(d->hs));
+            for (int w = 1; w < nw; ++w) pref[w] = pref[w - 1] + __builtin_popcount(mask[w - 1]);
+            // CRC register after message bit j and A-1-j zero bits (the register is
+            // linear in the message bits, utils.cpp:77-92): tab[A-1] = taps,
+            // tab[j] = one zero step of tab[j+1]
+            const int A = d->crc_n > 0 ? d->ca_A : 0;
+            std::vector<uint32_t> tab(std::max(A, 1), 0u);
+            if (A > 0) {
+                const uint32_t top = 1u << (d->crc_n - 1), msk = (top << 1) - 1u;
+                tab[A - 1] = d->crc_q & msk;
+                for (int j = A - 2; j >= 0; --j) {
+                    const uint32_t r = tab[j + 1];
+                    tab[j] = ((r << 1) & msk) ^ ((r & top) ? d->crc_q : 0u);
+                }
             }
+            int rc2 = upload(d->mc_pref, pref.data(), pref.size(), d->hs);
+            if (rc2) return rc2;
+            rc2 = upload(d->mc_crc, tab.data(), tab.size(), d->hs);
+            if (rc2) return rc2;
         }
-        int rc2 = upload(d->mc_pref, pref.data(), pref.size());
-        if (rc2) return rc2;
-        rc2 = upload(d->mc_crc, tab.data(), tab.size());
-        if (rc2) return rc2;
-    }
-    qpd::McChannel C;
-    std::memset(&C, 0, sizeof(C));
-    C.N = d->N;
-    C.K = d->K;
-    C.A = d->crc_n > 0 ? d->ca_A : d->K;
-    C.crc_n = d->crc_n;
-    C.q = ch->q;
-    C.n_edges = ch->n_edges;
-    C.seed_lo = (uint32_t)seed;
-    C.seed_hi = (uint32_t)(seed >> 32);
-    C.sigma = ch->sigma;
-    C.s2 = ch->sigma * ch->sigma;
-    C.info_mask = (const uint32_t *)d->info_mask.p;
-    C.info_pref = (const int32_t *)d->mc_pref.p;
-    C.crc_tab = (const uint32_t *)d->mc_crc.p;
-    for (int i = 0; i < ch->n_edges; ++i) C.edges[i] = ch->edges[i];
-    for (int i = 0; i + 1 < ch->n_edges; ++i) C.lut[i] = ch->lut[i];
-    int dev = 0, ncu = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    const int grid = (int)std::min<int64_t>(B, (int64_t)ncu * 32);
-    const size_t lds = qpd::mc_lds_bytes(d->N, d->K);
-    return timed_launch(d, QPD_KC_MC, (hipStream_t)stream, [&]() -> int {
-        hipLaunchKernelGGL(qpd::mc_frames_kernel, dim3(grid), dim3(64), lds, (hipStream_t)stream, C, frame0, B, d_msg,
-                           d_symbols);
-        QPD_HIP(hipGetLastError());
-        return QPD_OK;
+        qpd::McChannel C;
+        std::memset(&C, 0, sizeof(C));
+        C.N = d->N;
+        C.K = d->K;
+        C.A = d->crc_n > 0 ? d->ca_A : d->K;
+        C.crc_n = d->crc_n;
+        C.q = ch->q;
+        C.n_edges = ch->n_edges;
+        C.seed_lo = (uint32_t)seed;
+        C.seed_hi = (uint32_t)(seed >> 32);
+        C.sigma = ch->sigma;
+        C.s2 = ch->sigma * ch->sigma;
+        C.info_mask = (const uint32_t *)d->info_mask.p;
+        C.info_pref = (const int32_t *)d->mc_pref.p;
+        C.crc_tab = (const uint32_t *)d->mc_crc.p;
+        for (int i = 0; i < ch->n_edges; ++i) C.edges[i] = ch->edges[i];
+        for (int i = 0; i + 1 < ch->n_edges; ++i) C.lut[i] = ch->lut[i];
+        int dev = 0, ncu = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        const int grid = (int)std::min<int64_t>(B, (int64_t)ncu * 32);
+        const size_t lds = qpd::mc_lds_bytes(d->N, d->K);
+        return timed_launch(d, QPD_KC_MC, st, [&]() -> int {
+            hipLaunchKernelGGL(qpd::mc_frames_kernel, dim3(grid), dim3(64), lds, st, C, frame0, B, d_msg, d_symbols);
+            QPD_HIP(hipGetLastError());
+            return QPD_OK;
+        });
     });
 }
 
@@ -1268,12 +1400,14 @@ int qpd_probe_lds(int32_t device, int32_t op, double *gbps) {
 
 int qpd_profile(qpd_decoder *d, int32_t enable) {
     if (!d) return fail(QPD_E_INVALID, "null decoder");
+    std::lock_guard<std::mutex> lk(d->mu);
     d->prof = enable != 0;
     return QPD_OK;
 }
 
 int qpd_kernel_times(qpd_decoder *d, double *ms, int64_t *launches) {
     if (!d || !ms || !launches) return fail(QPD_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(d->mu);
     int rc = set_device(d);
     if (rc) return rc;
     for (int k = 0; k < QPD_KC_COUNT; ++k) {

@@ -28,21 +28,18 @@ struct Op {
 #define QPD_DYN 1  // tasks from a device queue (0: static grid-stride with evened rounds)
 #endif
 
-// One atomic per wave (lane 0, a vector atomic), the old value broadcast.
-__device__ __forceinline__ int64_t wave_take(uint32_t *ctr) {
+// One atomic per wave (lane 0, a vector atomic), the old value broadcast,
+// relative to the launch's base.  The counter is never reset: a launch of T
+// tasks on a grid of G <= T waves takes exactly T values (T - G successful
+// takes, then one failed take per wave), so the host advances the base by T
+// per launch (qpd_capi.hip: next_base) and the next launch on the decoder
+// starts where this one ended.  uint32 arithmetic: wrap-around is harmless.
+// Launches on one decoder are ordered by the host (stream events), so no
+// launch ever sees another's takes.
+__device__ __forceinline__ int64_t wave_take(uint32_t *ctr, uint32_t base) {
     uint32_t v = 0;
     if (threadIdx.x == 0) v = atomicAdd(ctr, 1u);
-    return (int64_t)__builtin_amdgcn_readfirstlane(v);
-}
-
-// The queue drains only after every wave has taken its last (failed) task;
-// the last wave out zeroes both counters ([0] taken, [1] done) for the next
-// launch.
-__device__ __forceinline__ void queue_done(uint32_t *ctr) {
-    if (QPD_DYN && wave_take(ctr + 1) == gridDim.x - 1 && threadIdx.x == 0) {
-        atomicExch(ctr, 0u);
-        atomicExch(ctr + 1, 0u);
-    }
+    return (int64_t)(uint32_t)(__builtin_amdgcn_readfirstlane(v) - base);
 }
 
 constexpr int kMaxDepth = 16;  // N <= 65536

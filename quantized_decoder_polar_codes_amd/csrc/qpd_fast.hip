@@ -87,7 +87,8 @@ struct FastPlan {
     const uint16_t *r1_rank;      // FastSCL R1 (<= 32 elements): [temp][v] rank << 1 | sign, per node at op.tab
     uint32_t *scratch;            // [waves][glb_rows][64]
     int32_t *err;
-    uint32_t *task_ctr;           // QPD_DYN task queue: [0] tasks taken, [1] waves done (both 0 between launches)
+    uint32_t *task_ctr;           // QPD_DYN task queue: tasks taken (never reset; see wave_take)
+    uint32_t task_base;           // per launch: the counter's value when this launch's takes begin
 };
 
 // Timing experiments only (wrong results): 0 = every op reads node 0's
@@ -1170,7 +1171,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
     // the queue -- every SIMD stays busy to the end whatever the residency --
     // or the grid-stride successor.
     for (int64_t task = blockIdx.x; task < ntasks;
-         task = QPD_DYN ? (int64_t)gridDim.x + wave_take(P.task_ctr) : task + gridDim.x) {
+         task = QPD_DYN ? (int64_t)gridDim.x + wave_take(P.task_ctr, P.task_base) : task + gridDim.x) {
 #ifdef QPD_POISON
         // Diagnosis builds only: every LDS word and slab row of this wave set to
         // QPD_POISON at the start of each task, so that a read of a row no op of
@@ -1489,7 +1490,6 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
         }
 #endif
     }
-    queue_done(P.task_ctr);
 }
 
 #ifndef QPD_FAST_TEMPLATES_ONLY  // qpd_fast_fscl.hip: the decode kernel templates only

@@ -72,7 +72,8 @@ struct DevPlan {
     const int32_t *info_pos;
     uint32_t *scratch;
     int32_t *err;
-    uint32_t *task_ctr;  // task queue ([0] taken, [1] waves done; 0 between launches)
+    uint32_t *task_ctr;  // task queue: groups taken (never reset; see wave_take)
+    uint32_t task_base;  // per launch: the counter's value when this launch's takes begin
 };
 
 __device__ __forceinline__ double vcl_at(const DevPlan &P, int row, int pos, int sym) {
@@ -358,7 +359,7 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
 
     // groups: the first blockIdx.x, then the next untaken one (qpd_common.hpp)
     for (int64_t grp = blockIdx.x; grp < ngroups;
-         grp = QPD_DYN ? (int64_t)gridDim.x + wave_take(P.task_ctr) : grp + gridDim.x) {
+         grp = QPD_DYN ? (int64_t)gridDim.x + wave_take(P.task_ctr, P.task_base) : grp + gridDim.x) {
         int64_t frame = grp * P.fpw + lane / gs;
         const bool frame_ok = frame < B;
         if (!frame_ok) frame = B - 1;
@@ -711,7 +712,6 @@ __global__ __launch_bounds__(64) void generic_decode_kernel(DevPlan P,
         }
         wave_sync();
     }
-    queue_done(P.task_ctr);
 }
 
 }  // namespace qpd

@@ -56,3 +56,65 @@ def oracle_mod():
 
     oracle.lib()
     return oracle
+
+
+def frame_lanes(info, frame):
+    """Where a frame runs in the kernels: (task, frame set, lanes).  Fast
+    engine: a task is frames_per_wave consecutive frames, set s holds
+    64 / lanes_per_frame of them, frame slot k of a set owns lanes
+    [k * lanes_per_frame, (k + 1) * lanes_per_frame)."""
+    fpw_task = int(info["frames_per_wave"])
+    gs = int(info["lanes_per_frame"])
+    per_set = max(1, 64 // gs)
+    slot = frame % fpw_task
+    k = slot % per_set
+    return frame // fpw_task, slot // per_set, (k * gs, (k + 1) * gs - 1)
+
+
+def assert_frames_equal(got, want, dec=None, label="", redecode=None, inputs=None):
+    """Bit-exact frame comparison that explains a mismatch instead of only
+    counting it: for each differing frame (up to 8) the task / frame set /
+    lanes it ran on, the differing bit positions and both bit strings; with
+    `redecode(rows) -> bits` the differing frames are decoded again, alone, in
+    a fresh decoder, which separates a deterministic difference (same result
+    alone) from one that depended on the run.  Everything is also written as
+    JSON to $QPD_DIAG_DIR (default gpurun_out/), which gpurun copies back."""
+    import json
+
+    got = np.asarray(got)
+    want = np.asarray(want)
+    assert got.shape == want.shape, (got.shape, want.shape)
+    bad = np.flatnonzero((got != want).reshape(len(got), -1).any(1))
+    if bad.size == 0:
+        return
+    info = dec.info() if dec is not None else None
+    rec = {"label": label, "frames": int(len(got)), "differing": bad.tolist(), "info": info, "detail": []}
+    alone = redecode(bad) if redecode is not None else None
+    lines = [f"{label}: {bad.size}/{len(got)} frames differ"]
+    for i, f in enumerate(bad[:8]):
+        pos = np.flatnonzero(got[f] != want[f])
+        d = {"frame": int(f), "bits_differ": pos.tolist(),
+             "got": "".join(map(str, got[f].astype(int))), "want": "".join(map(str, want[f].astype(int)))}
+        where = ""
+        if info is not None:
+            t, s, ln = frame_lanes(info, int(f))
+            d.update(task=t, set=s, lanes=list(ln))
+            where = f" (task {t}, set {s}, lanes {ln[0]}-{ln[1]})"
+        if alone is not None:
+            d["alone_equals_want"] = bool(np.array_equal(alone[i], want[f]))
+            d["alone_equals_got"] = bool(np.array_equal(alone[i], got[f]))
+        if inputs is not None:
+            d["input"] = np.asarray(inputs[f]).tolist()
+        rec["detail"].append(d)
+        lines.append(f"  frame {f}{where}: {pos.size} bits differ at {pos[:24].tolist()}"
+                     + ("" if alone is None else f"; alone in a fresh decoder: "
+                        f"{'= oracle' if d['alone_equals_want'] else ('= this run' if d['alone_equals_got'] else 'a third result')}"))
+    out_dir = os.environ.get("QPD_DIAG_DIR", os.path.join(ROOT, "gpurun_out"))
+    try:
+        os.makedirs(out_dir, exist_ok=True)
+        safe = "".join(c if c.isalnum() or c in "-_." else "_" for c in label)[:120] or "mismatch"
+        with open(os.path.join(out_dir, f"parity_fail_{safe}.json"), "w") as fh:
+            json.dump(rec, fh, indent=1)
+    except OSError:
+        pass
+    pytest.fail("\n".join(lines))

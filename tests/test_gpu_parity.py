@@ -15,7 +15,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import golden_files, golden_packed, load_golden
+from conftest import assert_frames_equal, golden_files, golden_packed, load_golden
 
 pytestmark = pytest.mark.gpu
 
@@ -58,8 +58,7 @@ def test_gpu_matches_golden(path, engine, qpd):
                               engine=engine, **kw)
         assert dec.info()["engine"] == (2 if engine == "auto" and L <= 8 else 1)  # L > 8: generic engine
         got = dec.decode_batch(g["symbols"].astype(np.int32))
-    bad = np.flatnonzero((got != g["expected"]).any(1))
-    assert bad.size == 0, f"{bad.size}/{len(got)} frames differ, first {bad[:5]}"
+    assert_frames_equal(got, g["expected"], dec, f"golden-{os.path.basename(path)[:-4]}-{engine}")
 
 
 CASES = [
@@ -114,8 +113,8 @@ def test_gpu_matches_oracle(N, K, L, tables, kind, engine, qpd, oracle_mod):
     if engine == "auto":
         assert dec.info()["engine"] == (1 if tables == "perelem" or (L > 8 and kind in ("SCL-LUT", "FastSCL-LUT")) else 2)
     got = dec.decode_batch(sym)
-    bad = np.flatnonzero((got != want).any(1))
-    assert bad.size == 0, f"{bad.size}/{B} frames differ, first {bad[:5]}"
+    redo = lambda rows: qpd.from_packed(kind, p, K, fm, L=L, node_type=nt, engine=engine).decode_batch(sym[rows])  # noqa: E731
+    assert_frames_equal(got, want, dec, f"oracle-{kind}-{N}-{K}-{L}-{tables}-{engine}", redo, sym)
 
 
 CA_CASES = [
@@ -165,8 +164,9 @@ def test_gpu_ca_matches_oracle(N, A, crc_n, L, tables, ebn0, kind, engine, qpd, 
     assert dec.info()["out_bits"] == A
     got = dec.decode_batch(sym)
     assert got.shape == (B, A)
-    bad = np.flatnonzero((got != want).any(1))
-    assert bad.size == 0, f"{bad.size}/{B} frames differ, first {bad[:5]}"
+    redo = lambda rows: qpd.from_packed(kind, p, K, fm, L=L, node_type=nt, engine=engine, A=A, crc_n=crc_n,  # noqa: E731
+                                        crc_loc=loc).decode_batch(sym[rows])
+    assert_frames_equal(got, want, dec, f"ca-{kind}-{N}-{A}-{crc_n}-{L}-{tables}-{engine}", redo, sym)
 
 
 def test_ca_dropin_api(qpd, oracle_mod):
@@ -352,8 +352,7 @@ def test_fastscl_rate1_paths(N, K, L, qpd, oracle_mod, monkeypatch):
             monkeypatch.setenv("QPD_LDS_BUDGET", str(budget))
         d = qpd.from_packed("FastSCL-LUT", p, K, fm, L=L, node_type=nt, engine="fast")
         got = d.decode_batch(sym)
-        bad = np.flatnonzero((got != want).any(1))
-        assert bad.size == 0, (budget, bad[:5])
+        assert_frames_equal(got, want, d, f"fscl-r1-{N}-{K}-{L}-budget{budget}", None, sym)
 
 
 def test_fast_engine_rejects_per_element_tables(qpd):
