@@ -329,10 +329,16 @@ def e2e_rate(args, ctx, wl):
     state = {"f0": wl.frame0 + (1 << 40)}  # frames never decoded by the throughput loop
     acc = torch.zeros(2, dtype=torch.int64, device=ctx.device)
 
+    fused = getattr(src, "decode_frames", None)  # qpd_mc_decode: generation feeds the decode kernel
+
     def step():
-        msg, sym = src(state["f0"], args.frames)
+        if fused is not None:
+            msg, bits = fused(state["f0"], args.frames)
+        else:  # a frame source without the fused call (the CPU tests' stand-in)
+            msg, sym = src(state["f0"], args.frames)
+            bits = dec.decode_batch(sym)
         state["f0"] += args.frames
-        e = (dec.decode_batch(sym) != msg).sum(1)
+        e = (bits != msg).sum(1)
         acc[0] += e.sum()
         acc[1] += (e > 0).sum()
 
@@ -346,11 +352,12 @@ def e2e_rate(args, ctx, wl):
     ctx.allreduce(tmax, dist.ReduceOp.MAX)
     frames = args.frames * args.steps * ctx.world
     r = {"value": frames / float(tmax.item()), "unit": "frames/s", "ms_per_step": float(tmax.item()) / args.steps * 1e3,
-         "what": "per step: qpd_mc_frames (Philox msg, encode, BPSK+AWGN, channel quantizer) + decode + error count"}
+         "what": "per step: qpd_mc_decode (Philox msg, encode, BPSK+AWGN, channel quantizer writing the decoder's root "
+                 "pre-pass rows, then the decode kernel) + error count"}
     if kt:
         mc_ms, n_mc = kt["mc"]
         r["mc_kernel_ms"] = mc_ms / max(1, n_mc)
-        r["mc_kernel_bytes"] = args.frames * (args.N * 4 + dec.out_bits)
+        r["mc_kernel_bytes"] = args.frames * (args.N + 2 * dec.out_bits)  # pre-pass rows (N B) + msg (K B) + bits
         r["mc_kernel_gbs"] = r["mc_kernel_bytes"] / (r["mc_kernel_ms"] * 1e-3) / 1e9
     return r
 
@@ -370,6 +377,7 @@ def mc_rank(args, ctx, wl):
     t0 = time.perf_counter()
     gloo = ctx.group is not None and dist.get_backend(ctx.group) == "gloo"
     r = MC.run_point(wl.src, dec.decode_batch, dec.K, args.ebn0, args.frames, F, stop, A=dec.out_bits,
+                     gen_decode=getattr(wl.src, "decode_frames", None),
                      group=ctx.group, count_device="cpu" if gloo else ctx.device)
     ctx.barrier()
     tmax = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=ctx.device)
@@ -455,8 +463,26 @@ def cpu_baseline(args, packed, fm, nt, sym, seconds, workers, A):
     shutil.rmtree(tmp, ignore_errors=True)
     wall = max(walls)
     return {"value": total / wall, "unit": "frames/s", "cores": workers, "kind": kind,
+            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "cores_note": f"{workers} worker processes = this GPU's CPU share (OMP_NUM_THREADS on the GPU box); "
+                          f"the machine shows {os.cpu_count()} CPUs shared by its 8 GPUs",
+            "build": "reference decoder sources compiled by oracle/build_ref.sh: g++ -O3 -DNDEBUG, the reference's "
+                     "Release flags without its -march=native (built in the container, run on this host)",
             "sample": f"{total} frames of the same workload (rank 0's first frames), {workers} worker processes x "
                       f"one decode() call per frame, {wall:.1f} s"}, outs
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or "unknown"
 
 
 def rank_job(args, ctx, make_workload):

@@ -191,9 +191,23 @@ int qpd_decode(qpd_decoder *dec, const int32_t *d_symbols, int64_t B, uint8_t *d
  * d_out: device uint8 [B][K] ([B][A] for QPD_CASCL_FLOAT). */
 int qpd_decode_f64(qpd_decoder *dec, const double *d_llr, int64_t B, uint8_t *d_out, void *stream);
 
-/* Host-buffer variants (synchronous). */
+/* Host-buffer variants (synchronous) -- what the reference's per-frame
+ * decode(symbols) call needs.  Small batches (qpd_info.host_max_frames; one
+ * frame per call in the reference drivers) run on the host engine, a C++
+ * decoder of this library for a few frames (no launch, copy or stream
+ * synchronization: SCLUTDecoder.cpp:21-124 costs ~10 us per frame on one core,
+ * a GPU call ~0.1 ms); larger batches on the GPU kernels.  Both decode the
+ * same bits (the reference's). */
 int qpd_decode_host(qpd_decoder *dec, const int32_t *h_symbols, int64_t B, uint8_t *h_out);
 int qpd_decode_f64_host(qpd_decoder *dec, const double *h_llr, int64_t B, uint8_t *h_out);
+
+/* Where the host-buffer calls run: AUTO (the default; the host engine up to
+ * qpd_info.host_max_frames frames, the GPU above), GPU (always), CPU (the host
+ * engine for every batch; QPD_E_UNSUPPORTED for the re-quantized float kinds,
+ * which the host engine does not decode).  The environment variable
+ * QPD_HOST_ENGINE=gpu|cpu sets it at create time. */
+enum qpd_host_mode { QPD_HOST_AUTO = 0, QPD_HOST_GPU = 1, QPD_HOST_CPU = 2 };
+int qpd_set_host_engine(qpd_decoder *dec, int32_t mode);
 
 /* Returns QPD_E_INPUT (and clears the flags) if any decode since the last
  * check saw a channel symbol outside [0, v), a Lloyd bisect index outside
@@ -224,6 +238,14 @@ typedef struct qpd_mc_channel {
 } qpd_mc_channel;
 int qpd_mc_frames(qpd_decoder *dec, const qpd_mc_channel *ch, uint64_t seed, int64_t frame0, int64_t B,
                   uint8_t *d_msg, int32_t *d_symbols, void *stream);
+/* The same frames, decoded: d_out = what qpd_decode returns for the symbols
+ * qpd_mc_frames generates with the same arguments (d_msg as there), without
+ * materializing the int32 symbols -- on a fast-engine decoder in pre-mode the
+ * generator writes the root pre-pass rows the decode kernel reads (LUT kinds;
+ * q <= v).  The driver's loop body (mainQuantizedDecoder_LLRDomain.py:151-178)
+ * in one call; the error count stays with the caller. */
+int qpd_mc_decode(qpd_decoder *dec, const qpd_mc_channel *ch, uint64_t seed, int64_t frame0, int64_t B,
+                  uint8_t *d_msg, uint8_t *d_out, void *stream);
 
 /*
  * Offline table design (host code, no device needed) -- the reference's
@@ -267,6 +289,8 @@ typedef struct qpd_info {
     int32_t lds_bytes_per_wave;
     int32_t lds_from_depth;   /* fast engine: tree depths >= this live in LDS */
     int32_t out_bits;         /* bits per decoded frame: K, or A (CRC-aided)  */
+    int64_t host_max_frames;  /* host-buffer calls of up to this many frames run
+                                 on the host engine (qpd_set_host_engine); 0: none */
 } qpd_info;
 int qpd_get_info(const qpd_decoder *dec, qpd_info *info);
 

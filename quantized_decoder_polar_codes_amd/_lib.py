@@ -35,14 +35,17 @@ EXPORTED = (
     "qpd_check_input_error",
     "qpd_get_info",
     "qpd_mc_frames",
+    "qpd_mc_decode",
     "qpd_optls_quantizer",
     "qpd_lutgen_mindistortion",
     "qpd_profile",
     "qpd_kernel_times",
     "qpd_probe_lds",
+    "qpd_set_host_engine",
 )
 QPD_KC_PRE, QPD_KC_DECODE, QPD_KC_MC, QPD_KC_COUNT = range(4)
 QPD_PROBE_BPERMUTE, QPD_PROBE_READ_B32, QPD_PROBE_READ_B64 = range(3)
+QPD_HOST_AUTO, QPD_HOST_GPU, QPD_HOST_CPU = range(3)
 
 _P = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -114,6 +117,7 @@ class QpdInfo(ctypes.Structure):
         ("lds_bytes_per_wave", _i32),
         ("lds_from_depth", _i32),
         ("out_bits", _i32),
+        ("host_max_frames", _i64),
     ]
 
 
@@ -164,6 +168,8 @@ def load():
     L.qpd_get_info.restype = ctypes.c_int
     L.qpd_mc_frames.argtypes = [_P, ctypes.POINTER(QpdMcChannel), ctypes.c_uint64, _i64, _i64, _P, _P, _P]
     L.qpd_mc_frames.restype = ctypes.c_int
+    L.qpd_mc_decode.argtypes = [_P, ctypes.POINTER(QpdMcChannel), ctypes.c_uint64, _i64, _i64, _P, _P, _P]
+    L.qpd_mc_decode.restype = ctypes.c_int
     L.qpd_optls_quantizer.argtypes = [_P, _P, _i32, _i32, _i32, _P, _P, _P, _P]
     L.qpd_optls_quantizer.restype = ctypes.c_int
     L.qpd_lutgen_mindistortion.argtypes = [_i32, _i32, _P, _P, _i32, _i32, _P, _P, _P, _P]
@@ -174,6 +180,8 @@ def load():
     L.qpd_kernel_times.restype = ctypes.c_int
     L.qpd_probe_lds.argtypes = [_i32, _i32, ctypes.POINTER(ctypes.c_double)]
     L.qpd_probe_lds.restype = ctypes.c_int
+    L.qpd_set_host_engine.argtypes = [_P, _i32]
+    L.qpd_set_host_engine.restype = ctypes.c_int
     if L.qpd_abi_version() != ABI_VERSION:
         raise ImportError("libqpd.so ABI version mismatch")
     L.qpd_build_id.restype = ctypes.c_char_p

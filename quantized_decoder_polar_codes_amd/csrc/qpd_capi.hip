@@ -20,6 +20,10 @@ const void *fast_kernel_fscl(int sets, bool l8, bool r1l);  // qpd_fast_fscl.hip
 }
 #include "qpd_mc.hip"
 #include "qpd_probe.hip"
+#include "qpd_host.hpp"
+#include "qpd_schedule.hpp"
+
+#include <memory>
 
 namespace {
 
@@ -38,60 +42,16 @@ int fail(int code, const std::string &msg) {
 
 using qpd::DevPlan;
 using qpd::Op;
+using qpd_sched::Schedule;
+using qpd_sched::special_of;
+using qpd_sched::visit;
+using qpd_sched::family_of;
+using qpd_sched::is_ca;
 
 int ilog2_exact(int N) {
     int n = 0;
     while ((1 << n) < N) ++n;
     return ((1 << n) == N) ? n : -1;
-}
-
-// Static traversal schedule.  The reference walks the
-// tree with a node_state machine (src/SCLLUTDecoder.cpp:62-243); the walk does
-// not depend on data, so it is compiled once per code into a flat op list that
-// every frame replays.  Special nodes follow node_type AS PASSED (H7):
-// FastSC-LUT handles R0/R1/REP/SPC (FastSCLUT.cpp:46-107), FastSCL-LUT handles
-// R0/R1/REP only (FastSCLLUTDecoder.cpp:82-215); other labels decode as plain
-// f/g nodes.
-struct Schedule {
-    std::vector<Op> ops;
-    int max_r1 = 0;
-};
-
-int special_of(int kind, const int32_t *node_type, int posi) {
-    if (!node_type) return -1;
-    const int t = node_type[posi];
-    if (kind == QPD_FASTSC_LUT && t >= 0 && t <= 3) return t;
-    if (kind == QPD_FASTSCL_LUT && t >= 0 && t <= 2) return t;
-    return -1;
-}
-
-void emit(Schedule &s, int type, int d, int node, int aux) {
-    Op op;
-    op.type = type;
-    op.d = d;
-    op.node = node;
-    op.aux = aux;
-    s.ops.push_back(op);
-}
-
-void visit(Schedule &s, int kind, int N, int n, const int32_t *frozen, const int32_t *node_type, int d, int node) {
-    const int posi = (1 << d) + node - 1;
-    const int t = special_of(kind, node_type, posi);
-    if (t >= 0) {
-        emit(s, qpd::OP_R0 + t, d, node, 0);
-        if (t == 1) s.max_r1 = std::max(s.max_r1, N >> d);
-        return;
-    }
-    if (d + 1 < n) {
-        emit(s, qpd::OP_F, d, node, 0);
-        visit(s, kind, N, n, frozen, node_type, d + 1, 2 * node);
-        emit(s, qpd::OP_G, d, node, 0);
-        visit(s, kind, N, n, frozen, node_type, d + 1, 2 * node + 1);
-    } else {
-        emit(s, qpd::OP_LEAF_L, d, node, frozen[2 * node] == 1);
-        emit(s, qpd::OP_LEAF_R, d, node, frozen[2 * node + 1] == 1);
-    }
-    emit(s, qpd::OP_COMB, d, node, 0);
 }
 
 struct DeviceBuf {
@@ -123,6 +83,8 @@ struct qpd_decoder {
     int64_t pre_chunk = 0;    // frames per pre-pass chunk
     int64_t pre_cap = 0;      // frames pre_buf holds
     DeviceBuf pre_buf;
+    DeviceBuf mc_sym;        // qpd_mc_decode without a fused pre-pass: int32 symbols of one chunk
+    int64_t mc_sym_cap = 0;  // frames mc_sym holds
     DevPlan plan{};
     qpd::FastPlan fplan{};
     DeviceBuf f_tab, g_tab, fscratch, mops, r1_rank, task_ctr;
@@ -151,6 +113,14 @@ struct qpd_decoder {
     hipStream_t last_st = nullptr;
     bool last_valid = false;
     uint32_t task_base = 0;  // task queue counter at the start of the next launch (wave_take)
+    // Host engine (qpd_host.hpp) for the host-buffer entry points' small
+    // batches: the per-frame drop-in call.  Null for the kinds it does not
+    // decode (re-quantized float domains).
+    std::unique_ptr<qpd_host::Plan> hplan;
+    std::unique_ptr<qpd_host::Engine<uint8_t>> heng_lut;
+    std::unique_ptr<qpd_host::Engine<double>> heng_f64;
+    int host_mode = QPD_HOST_AUTO;
+    int64_t host_max_frames = 0;  // QPD_HOST_AUTO: batches up to this size run on the host engine
     // qpd_profile: HIP events around every launch, per kernel class
     bool prof = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[QPD_KC_COUNT];
@@ -238,30 +208,6 @@ int timed_launch(qpd_decoder *d, int kc, hipStream_t st, F &&launch) {
 // Kernel family (SC / SCL / FastSC / FastSCL, as the LUT kind ids) and symbol
 // domain of every public kind; the CRC-aided kinds are their list family
 // plus an output epilogue.
-bool family_of(int kind, int *fam, int *dom) {
-    using namespace qpd;
-    switch (kind) {
-        case QPD_SC_FLOAT: *fam = QPD_SC_LUT; *dom = DOM_FLOAT; return true;
-        case QPD_SC_LUT:
-        case QPD_SCL_LUT:
-        case QPD_FASTSC_LUT:
-        case QPD_FASTSCL_LUT: *fam = kind; *dom = DOM_LUT; return true;
-        case QPD_CASCL_LUT: *fam = QPD_SCL_LUT; *dom = DOM_LUT; return true;
-        case QPD_CAFASTSCL_LUT: *fam = QPD_FASTSCL_LUT; *dom = DOM_LUT; return true;
-        case QPD_SCL_FLOAT:
-        case QPD_CASCL_FLOAT: *fam = QPD_SCL_LUT; *dom = DOM_FLOAT; return true;
-        case QPD_FASTSC_FLOAT: *fam = QPD_FASTSC_LUT; *dom = DOM_FLOAT; return true;
-        case QPD_FASTSCL_FLOAT: *fam = QPD_FASTSCL_LUT; *dom = DOM_FLOAT; return true;
-        case QPD_SC_UNIFORM: *fam = QPD_SC_LUT; *dom = DOM_UNIFORM; return true;
-        case QPD_SCL_UNIFORM: *fam = QPD_SCL_LUT; *dom = DOM_UNIFORM; return true;
-        case QPD_SC_LLOYD: *fam = QPD_SC_LUT; *dom = DOM_LLOYD; return true;
-        case QPD_SCL_LLOYD: *fam = QPD_SCL_LUT; *dom = DOM_LLOYD; return true;
-        default: return false;
-    }
-}
-
-bool is_ca(int kind) { return kind == QPD_CASCL_LUT || kind == QPD_CAFASTSCL_LUT || kind == QPD_CASCL_FLOAT; }
-
 int validate(const qpd_config *c, int *n_out, int *fam_out, int *dom_out) {
     if (!c) return fail(QPD_E_INVALID, "null config");
     int fam = 0, dom = 0;
@@ -852,6 +798,39 @@ int launch_generic(qpd_decoder *d, const In *in, int64_t B, uint8_t *out, int gr
     return rc;
 }
 
+// The host engine's copy of the plan (qpd_host.hpp) and the batch size up to
+// which QPD_HOST_AUTO prefers it.  The crossover is a cost model fitted to the
+// per-call latencies measured on MI355X (tools/latency.py,
+// profiles/r03_latency.jsonl): a GPU call costs a fixed launch / copy /
+// synchronization overhead plus one wave running the whole serial schedule,
+// whatever the batch up to thousands of frames; the host engine costs its
+// per-frame work times the batch.
+int build_host(qpd_decoder *d, const qpd_config *cfg, size_t nops) {
+    std::unique_ptr<qpd_host::Plan> h = qpd_host::make_plan(cfg);
+    if (!h) return QPD_OK;  // re-quantized float kinds: GPU only
+    if (h->dom == qpd::DOM_LUT)
+        d->heng_lut = std::make_unique<qpd_host::Engine<uint8_t>>(*h);
+    else
+        d->heng_f64 = std::make_unique<qpd_host::Engine<double>>(*h);
+    // Per frame on the host engine ~ its lookups (N log2 N per path) plus,
+    // for lists, the forks (measured: SC-LUT N=128 4.5 us, N=1024 46 us,
+    // SCL-LUT N=1024 L=8 0.57 ms); a GPU call ~ 55 us of launches, copies
+    // and synchronization plus one wave running the serial schedule
+    // (SC-LUT N=128 0.11 ms, N=1024 0.91 ms, SCL-LUT N=1024 L=8 1.06 ms,
+    // profiles/r02_latency.jsonl) -- flat in the batch up to thousands of frames.
+    const double nn = (double)h->N * h->n;
+    const double host_us = 0.004 * nn * h->L + (h->L > 1 ? 0.05 * h->L * h->N : 0.0) + 1.0;
+    const double gpu_us = 55.0 + 0.083 * nn + (h->L > 1 ? 0.02 * nn : 0.0);
+    (void)nops;
+    d->host_max_frames = std::max<int64_t>(1, (int64_t)(gpu_us / host_us));
+    d->hplan = std::move(h);
+    if (const char *e = getenv("QPD_HOST_ENGINE")) {
+        if (!strcmp(e, "gpu")) d->host_mode = QPD_HOST_GPU;
+        if (!strcmp(e, "cpu")) d->host_mode = QPD_HOST_CPU;
+    }
+    return QPD_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1067,6 +1046,13 @@ int qpd_create(const qpd_config *cfg, qpd_decoder **out) {
     d->fplan.crc_n = d->crc_n;
     d->fplan.crc_q = d->crc_q;
     d->fplan.info_mask = (const uint32_t *)d->info_mask.p;
+    {
+        const int rc = build_host(d, cfg, s.ops.size());
+        if (rc) {
+            delete d;
+            return rc;
+        }
+    }
     *out = d;
     return QPD_OK;
 }
@@ -1081,6 +1067,8 @@ int qpd_get_info(const qpd_decoder *d, qpd_info *info) {
     if (!d || !info) return fail(QPD_E_INVALID, "null argument");
     info->kind = d->pub_kind;
     info->out_bits = d->out_bits;
+    info->host_max_frames = !d->hplan ? 0 : d->host_mode == QPD_HOST_GPU ? 0
+                            : d->host_mode == QPD_HOST_CPU ? INT64_MAX : d->host_max_frames;
     info->N = d->N;
     info->K = d->K;
     info->L = d->L;
@@ -1102,85 +1090,178 @@ namespace {
 
 // Launches of one device-buffer decode on stream st (caller: lock held,
 // stream ordered).
+// One fast-engine decode launch over Bc frames whose rows start at `in`
+// (channel symbols, in_shift = n; or pre-pass rows, in_shift = n - 2).
+int fast_launch(qpd_decoder *d, qpd::FastPlan fp, const int32_t *in, int64_t Bc, uint8_t *out, hipStream_t st) {
+    const int64_t tw = (int64_t)d->fplan.fpw * d->sets;  // frames per wave task
+    const void *kfn = fast_kernel(d->kind, d->sets, d->l8, d->r1l);
+    if (!kfn) return fail(QPD_E_INVALID, "bad kind");
+    const int64_t fgroups = (Bc + tw - 1) / tw;
+    int fgrid = (int)std::min<int64_t>(fgroups, d->max_waves);
+    if (!QPD_DYN) {
+        // even out the rounds of the grid-stride loop (no partial last round)
+        const int64_t rounds = (fgroups + fgrid - 1) / fgrid;
+        fgrid = (int)((fgroups + rounds - 1) / rounds);
+    }
+    const qpd::MOp *ops_arg = fp.ops;
+    fp.task_base = d->task_base;
+    void *args[] = {&fp, &in, &Bc, &out, &ops_arg};
+    const size_t lds = (size_t)d->lds_bytes;
+    const int rc = timed_launch(d, QPD_KC_DECODE, st, [&]() -> int {
+        QPD_HIP(hipLaunchKernel(kfn, dim3(fgrid), dim3(64), args, lds, st));
+        QPD_HIP(hipGetLastError());
+        return QPD_OK;
+    });
+    if (!rc) d->task_base += (uint32_t)fgroups;  // takes of this launch (wave_take)
+    return rc;
+}
+
+// The decode of Bc frames from their root pre-pass rows (pre-mode decoders).
+int decode_pre_rows(qpd_decoder *d, const uint32_t *rows, int64_t Bc, uint8_t *out, hipStream_t st) {
+    qpd::FastPlan fp = d->fplan;
+    fp.in_vec = 1;
+    fp.in_shift = fp.n - 2;
+    return fast_launch(d, fp, (const int32_t *)rows, Bc, out, st);
+}
+
+// pre-pass rows for `chunk` frames (N bytes each), grown on demand; on an
+// allocation failure the chunk halves (fewer frames per decode launch, same
+// results).  Returns the frames the buffer holds.
+int64_t ensure_pre_rows(qpd_decoder *d, int64_t chunk, int *rc) {
+    *rc = QPD_OK;
+    if (d->pre_cap >= chunk) return std::min<int64_t>(chunk, d->pre_cap);
+    if (d->pre_buf.p) (void)hipFree(d->pre_buf.p);
+    d->pre_buf.p = nullptr;
+    d->pre_cap = 0;
+    hipError_t e = hipErrorOutOfMemory;
+    while (chunk >= 1 && (e = hipMalloc(&d->pre_buf.p, (size_t)chunk * (size_t)d->N)) != hipSuccess) {
+        (void)hipGetLastError();
+        d->pre_buf.p = nullptr;
+        chunk /= 2;
+    }
+    if (e != hipSuccess) {
+        *rc = fail(QPD_E_DEVICE, std::string("pre-pass rows hipMalloc: ") + hipGetErrorString(e));
+        return 0;
+    }
+    d->pre_cap = chunk;
+    return chunk;
+}
+
+// Launches of one device-buffer decode on stream st (caller: lock held,
+// stream ordered).
 int decode_impl(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_out, hipStream_t st) {
     int rc = QPD_OK;
-    const int64_t groups = (B + d->plan.fpw - 1) / d->plan.fpw;
-    const int grid = (int)std::min<int64_t>(groups, d->max_waves);
-    if (d->engine == QPD_ENGINE_FAST) {
-        const int64_t tw = (int64_t)d->fplan.fpw * d->sets;  // frames per wave task
-        const size_t lds = (size_t)d->lds_bytes;
-        qpd::FastPlan fp = d->fplan;
-        fp.in_vec = ((uintptr_t)d_symbols & 15u) == 0 && (fp.N & 3) == 0;
-        const void *kfn = fast_kernel(d->kind, d->sets, d->l8, d->r1l);
-        if (!kfn) return fail(QPD_E_INVALID, "bad kind");
-        auto decode = [&](const int32_t *in_arg, int64_t Bc, uint8_t *out_arg) -> int {
-            const int64_t fgroups = (Bc + tw - 1) / tw;
-            int fgrid = (int)std::min<int64_t>(fgroups, d->max_waves);
-            if (!QPD_DYN) {
-                // even out the rounds of the grid-stride loop (no partial last round)
-                const int64_t rounds = (fgroups + fgrid - 1) / fgrid;
-                fgrid = (int)((fgroups + rounds - 1) / rounds);
-            }
-            const qpd::MOp *ops_arg = fp.ops;
-            fp.task_base = d->task_base;
-            void *args[] = {&fp, &in_arg, &Bc, &out_arg, &ops_arg};
-            const int lrc = timed_launch(d, QPD_KC_DECODE, st, [&]() -> int {
-                QPD_HIP(hipLaunchKernel(kfn, dim3(fgrid), dim3(64), args, lds, st));
-                QPD_HIP(hipGetLastError());
-                return QPD_OK;
-            });
-            if (!lrc) d->task_base += (uint32_t)fgroups;  // takes of this launch (wave_take)
-            return lrc;
-        };
-        if (!d->pre) {
-            fp.in_shift = fp.n;
-            return decode(d_symbols, B, d_out);
-        }
-        // pre-mode: root pre-pass, then the decode on its rows, chunk by chunk
-        int64_t chunk = std::min<int64_t>(B, d->pre_chunk);
-        if (d->pre_cap < chunk) {
-            if (d->pre_buf.p) QPD_HIP(hipFree(d->pre_buf.p));
-            d->pre_buf.p = nullptr;
-            d->pre_cap = 0;
-            // N bytes per frame; on an allocation failure the chunk halves
-            // (fewer frames per decode launch, same results)
-            hipError_t e = hipErrorOutOfMemory;
-            while (chunk >= 1 && (e = hipMalloc(&d->pre_buf.p, (size_t)chunk * (size_t)fp.N)) != hipSuccess) {
-                (void)hipGetLastError();
-                d->pre_buf.p = nullptr;
-                chunk /= 2;
-            }
-            if (e != hipSuccess) return fail(QPD_E_DEVICE, std::string("pre-pass rows hipMalloc: ") + hipGetErrorString(e));
-            d->pre_cap = chunk;
-        }
-        chunk = std::min<int64_t>(chunk, d->pre_cap);
-        uint32_t *pre = (uint32_t *)d->pre_buf.p;
-        for (int64_t f0 = 0; f0 < B; f0 += chunk) {
-            int64_t Bc = std::min<int64_t>(chunk, B - f0);
-            const int32_t *sym = d_symbols + f0 * fp.N;
-            fp.in_shift = fp.n;
-            const int pgrid = (int)std::min<int64_t>(((Bc << (fp.n - 4)) + 255) / 256, 8192);
-            void *pargs[] = {&fp, &sym, &Bc, &pre};
-            rc = timed_launch(d, QPD_KC_PRE, st, [&]() -> int {
-                QPD_HIP(hipLaunchKernel(reinterpret_cast<const void *>(&qpd::root_pre_kernel), dim3(pgrid), dim3(256),
-                                        pargs, 0, st));
-                QPD_HIP(hipGetLastError());
-                return QPD_OK;
-            });
-            if (rc) return rc;
-            fp.in_shift = fp.n - 2;
-            rc = decode((const int32_t *)pre, Bc, d_out + f0 * fp.out_k);
-            if (rc) return rc;
-        }
-        return QPD_OK;
+    if (d->engine != QPD_ENGINE_FAST) {
+        const int64_t groups = (B + d->plan.fpw - 1) / d->plan.fpw;
+        return launch_generic(d, d_symbols, B, d_out, (int)std::min<int64_t>(groups, d->max_waves), st);
     }
-    return launch_generic(d, d_symbols, B, d_out, grid, st);
+    qpd::FastPlan fp = d->fplan;
+    fp.in_vec = ((uintptr_t)d_symbols & 15u) == 0 && (fp.N & 3) == 0;
+    if (!d->pre) {
+        fp.in_shift = fp.n;
+        return fast_launch(d, fp, d_symbols, B, d_out, st);
+    }
+    // pre-mode: root pre-pass, then the decode on its rows, chunk by chunk
+    const int64_t chunk = ensure_pre_rows(d, std::min<int64_t>(B, d->pre_chunk), &rc);
+    if (rc) return rc;
+    uint32_t *pre = (uint32_t *)d->pre_buf.p;
+    for (int64_t f0 = 0; f0 < B; f0 += chunk) {
+        int64_t Bc = std::min<int64_t>(chunk, B - f0);
+        const int32_t *sym = d_symbols + f0 * fp.N;
+        fp.in_shift = fp.n;
+        const int pgrid = (int)std::min<int64_t>(((Bc << (fp.n - 4)) + 255) / 256, 8192);
+        void *pargs[] = {&fp, &sym, &Bc, &pre};
+        rc = timed_launch(d, QPD_KC_PRE, st, [&]() -> int {
+            QPD_HIP(hipLaunchKernel(reinterpret_cast<const void *>(&qpd::root_pre_kernel), dim3(pgrid), dim3(256),
+                                    pargs, 0, st));
+            QPD_HIP(hipGetLastError());
+            return QPD_OK;
+        });
+        if (rc) return rc;
+        rc = decode_pre_rows(d, pre, Bc, d_out + f0 * fp.out_k, st);
+        if (rc) return rc;
+    }
+    return QPD_OK;
 }
 
 int decode_f64_impl(qpd_decoder *d, const double *d_llr, int64_t B, uint8_t *d_out, hipStream_t st) {
     const int64_t groups = (B + d->plan.fpw - 1) / d->plan.fpw;
     const int grid = (int)std::min<int64_t>(groups, d->max_waves);
     return launch_generic(d, d_llr, B, d_out, grid, st);
+}
+
+int check_channel(const qpd_mc_channel *ch) {
+    if (ch->n_edges < 2 || ch->n_edges > qpd::kMcMaxEdges) return fail(QPD_E_INVALID, "n_edges must be in [2, 257]");
+    if (!ch->edges || !ch->lut) return fail(QPD_E_INVALID, "null channel quantizer");
+    if (!(ch->sigma > 0) || ch->q < 2) return fail(QPD_E_INVALID, "sigma must be > 0 and q >= 2");
+    for (int i = 0; i + 1 < ch->n_edges; ++i) {
+        if (!(ch->edges[i] <= ch->edges[i + 1])) return fail(QPD_E_INVALID, "edges must be ascending");
+        if (ch->lut[i] < 0 || ch->lut[i] >= ch->q) return fail(QPD_E_INVALID, "lut entry outside [0, q)");
+    }
+    return QPD_OK;
+}
+
+// The Monte-Carlo generator on stream st: int32 symbols to `rows`, or (pre)
+// the decoder's root pre-pass rows.  Caller: lock held, stream ordered.
+int mc_launch(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64_t frame0, int64_t B, uint8_t *d_msg,
+              int32_t *rows, bool pre, hipStream_t st) {
+    if (!d->mc_pref.p) {  // per-decoder constants of the generator, built at the first call
+        const int nw = (d->N + 31) / 32;
+        std::vector<int32_t> pref(nw, 0);
+        std::vector<uint32_t> mask(nw, 0u);
+        QPD_HIP(hipMemcpyAsync(mask.data(), d->info_mask.p, nw * sizeof(uint32_t), hipMemcpyDeviceToHost, d->hs));
+        QPD_HIP(hipStreamSynchronize(d->hs));
+        for (int w = 1; w < nw; ++w) pref[w] = pref[w - 1] + __builtin_popcount(mask[w - 1]);
+        // CRC register after message bit j and A-1-j zero bits (the register is
+        // linear in the message bits, utils.cpp:77-92): tab[A-1] = taps,
+        // tab[j] = one zero step of tab[j+1]
+        const int A = d->crc_n > 0 ? d->ca_A : 0;
+        std::vector<uint32_t> tab(std::max(A, 1), 0u);
+        if (A > 0) {
+            const uint32_t top = 1u << (d->crc_n - 1), msk = (top << 1) - 1u;
+            tab[A - 1] = d->crc_q & msk;
+            for (int j = A - 2; j >= 0; --j) {
+                const uint32_t r = tab[j + 1];
+                tab[j] = ((r << 1) & msk) ^ ((r & top) ? d->crc_q : 0u);
+            }
+        }
+        int rc2 = upload(d->mc_pref, pref.data(), pref.size(), d->hs);
+        if (rc2) return rc2;
+        rc2 = upload(d->mc_crc, tab.data(), tab.size(), d->hs);
+        if (rc2) return rc2;
+    }
+    qpd::McChannel C;
+    std::memset(&C, 0, sizeof(C));
+    C.N = d->N;
+    C.K = d->K;
+    C.A = d->crc_n > 0 ? d->ca_A : d->K;
+    C.crc_n = d->crc_n;
+    C.q = ch->q;
+    C.n_edges = ch->n_edges;
+    C.seed_lo = (uint32_t)seed;
+    C.seed_hi = (uint32_t)(seed >> 32);
+    C.sigma = ch->sigma;
+    C.s2 = ch->sigma * ch->sigma;
+    C.info_mask = (const uint32_t *)d->info_mask.p;
+    C.info_pref = (const int32_t *)d->mc_pref.p;
+    C.crc_tab = (const uint32_t *)d->mc_crc.p;
+    C.f_tab = d->fplan.f_tab;
+    C.g_tab = d->fplan.g_tab;
+    for (int i = 0; i < ch->n_edges; ++i) C.edges[i] = ch->edges[i];
+    for (int i = 0; i + 1 < ch->n_edges; ++i) C.lut[i] = ch->lut[i];
+    int dev = 0, ncu = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int grid = (int)std::min<int64_t>(B, (int64_t)ncu * 32);
+    const size_t lds = qpd::mc_lds_bytes(d->N, d->K, pre);
+    return timed_launch(d, QPD_KC_MC, st, [&]() -> int {
+        if (pre)
+            hipLaunchKernelGGL(qpd::mc_frames_kernel<true>, dim3(grid), dim3(64), lds, st, C, frame0, B, d_msg, rows);
+        else
+            hipLaunchKernelGGL(qpd::mc_frames_kernel<false>, dim3(grid), dim3(64), lds, st, C, frame0, B, d_msg, rows);
+        QPD_HIP(hipGetLastError());
+        return QPD_OK;
+    });
 }
 
 // One call's work on stream st, ordered after the decoder's previous work on
@@ -1246,6 +1327,23 @@ static int ensure(DeviceBuf &b, size_t &have, size_t need) {
 // H2D copy, decode and D2H copies of the bits and the error word queued on
 // the handle's own stream, one stream synchronization.  (What a per-frame
 // decode(symbols) call of the reference drivers costs here: tools/latency.py.)
+// Whether a host-buffer call of B frames runs on the host engine.
+static bool host_engine_takes(const qpd_decoder *d, int64_t B) {
+    if (!d->hplan || d->host_mode == QPD_HOST_GPU) return false;
+    return d->host_mode == QPD_HOST_CPU || B <= d->host_max_frames;
+}
+
+// B frames on the host engine, one after another, under the handle's lock.
+// The GPU work of the decoder is not touched (the engine has its own state),
+// so no stream ordering is needed.
+template <class Eng, class In>
+static int host_engine_run(qpd_decoder *d, Eng *eng, const In *h_in, int64_t B, uint8_t *h_out) {
+    std::lock_guard<std::mutex> lk(d->mu);
+    int32_t flag = 0;
+    for (int64_t b = 0; b < B; ++b) flag |= eng->decode(h_in + b * d->N, h_out + b * d->out_bits);
+    return flag ? input_error(flag) : QPD_OK;
+}
+
 template <class In, class Dec>
 static int host_roundtrip(qpd_decoder *d, const In *h_in, int64_t B, uint8_t *h_out, Dec dec) {
     const size_t in_b = (size_t)B * d->N * sizeof(In), out_b = (size_t)B * d->out_bits;
@@ -1308,6 +1406,7 @@ int qpd_decode_host(qpd_decoder *d, const int32_t *h_symbols, int64_t B, uint8_t
     if (d->dom != qpd::DOM_LUT) return fail(QPD_E_INVALID, "this decoder takes float64 LLRs: use qpd_decode_f64_host");
     if (B <= 0) return B == 0 ? QPD_OK : fail(QPD_E_INVALID, "negative batch");
     if (!h_symbols || !h_out) return fail(QPD_E_INVALID, "null buffer");
+    if (host_engine_takes(d, B)) return host_engine_run(d, d->heng_lut.get(), h_symbols, B, h_out);
     return host_roundtrip(d, h_symbols, B, h_out,
                           [&](const int32_t *in, uint8_t *out, hipStream_t st) { return decode_impl(d, in, B, out, st); });
 }
@@ -1317,8 +1416,19 @@ int qpd_decode_f64_host(qpd_decoder *d, const double *h_llr, int64_t B, uint8_t 
     if (d->dom == qpd::DOM_LUT) return fail(QPD_E_INVALID, "LUT decoders take int32 channel symbols: use qpd_decode_host");
     if (B <= 0) return B == 0 ? QPD_OK : fail(QPD_E_INVALID, "negative batch");
     if (!h_llr || !h_out) return fail(QPD_E_INVALID, "null buffer");
+    if (host_engine_takes(d, B)) return host_engine_run(d, d->heng_f64.get(), h_llr, B, h_out);
     return host_roundtrip(d, h_llr, B, h_out,
                           [&](const double *in, uint8_t *out, hipStream_t st) { return decode_f64_impl(d, in, B, out, st); });
+}
+
+int qpd_set_host_engine(qpd_decoder *d, int32_t mode) {
+    if (!d) return fail(QPD_E_INVALID, "null decoder");
+    if (mode < QPD_HOST_AUTO || mode > QPD_HOST_CPU) return fail(QPD_E_INVALID, "mode must be QPD_HOST_AUTO, _GPU or _CPU");
+    if (mode == QPD_HOST_CPU && !d->hplan)
+        return fail(QPD_E_UNSUPPORTED, "the host engine does not decode the re-quantized float kinds");
+    std::lock_guard<std::mutex> lk(d->mu);
+    d->host_mode = mode;
+    return QPD_OK;
 }
 
 int qpd_mc_frames(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64_t frame0, int64_t B, uint8_t *d_msg,
@@ -1327,67 +1437,53 @@ int qpd_mc_frames(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64
     if (B < 0 || frame0 < 0) return fail(QPD_E_INVALID, "negative frame range");
     if (B == 0) return QPD_OK;
     if (!d_msg || !d_symbols) return fail(QPD_E_INVALID, "null buffer");
-    if (ch->n_edges < 2 || ch->n_edges > qpd::kMcMaxEdges) return fail(QPD_E_INVALID, "n_edges must be in [2, 257]");
-    if (!ch->edges || !ch->lut) return fail(QPD_E_INVALID, "null channel quantizer");
-    if (!(ch->sigma > 0) || ch->q < 2) return fail(QPD_E_INVALID, "sigma must be > 0 and q >= 2");
-    for (int i = 0; i + 1 < ch->n_edges; ++i) {
-        if (!(ch->edges[i] <= ch->edges[i + 1])) return fail(QPD_E_INVALID, "edges must be ascending");
-        if (ch->lut[i] < 0 || ch->lut[i] >= ch->q) return fail(QPD_E_INVALID, "lut entry outside [0, q)");
-    }
+    int rc = check_channel(ch);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    return ordered(d, st, [&]() { return mc_launch(d, ch, seed, frame0, B, d_msg, d_symbols, false, st); });
+}
+
+int qpd_mc_decode(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64_t frame0, int64_t B, uint8_t *d_msg,
+                  uint8_t *d_out, void *stream) {
+    if (!d || !ch) return fail(QPD_E_INVALID, "null argument");
+    if (d->dom != qpd::DOM_LUT) return fail(QPD_E_INVALID, "qpd_mc_decode needs a LUT decoder (int32 channel symbols)");
+    if (B < 0 || frame0 < 0) return fail(QPD_E_INVALID, "negative frame range");
+    if (B == 0) return QPD_OK;
+    if (!d_msg || !d_out) return fail(QPD_E_INVALID, "null buffer");
+    int rc = check_channel(ch);
+    if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
     return ordered(d, st, [&]() -> int {
-        if (!d->mc_pref.p) {  // per-decoder constants of the generator, built at the first call
-            const int nw = (d->N + 31) / 32;
-            std::vector<int32_t> pref(nw, 0);
-            std::vector<uint32_t> mask(nw, 0u);
-            QPD_HIP(hipMemcpyAsync(mask.data(), d->info_mask.p, nw * sizeof(uint32_t), hipMemcpyDeviceToHost, d->hs));
-            QPD_HIP(hipStreamSynchronize(d->hs));
-            for (int w = 1; w < nw; ++w) pref[w] = pref[w - 1] + __builtin_popcount(mask[w - 1]);
-            // CRC register after message bit j and A-1-j zero bits (the register is
-            // linear in the message bits, utils.cpp:77-92): tab[A-1] = taps,
-            // tab[j] = one zero step of tab[j+1]
-            const int A = d->crc_n > 0 ? d->ca_A : 0;
-            std::vector<uint32_t> tab(std::max(A, 1), 0u);
-            if (A > 0) {
-                const uint32_t top = 1u << (d->crc_n - 1), msk = (top << 1) - 1u;
-                tab[A - 1] = d->crc_q & msk;
-                for (int j = A - 2; j >= 0; --j) {
-                    const uint32_t r = tab[j + 1];
-                    tab[j] = ((r << 1) & msk) ^ ((r & top) ? d->crc_q : 0u);
-                }
+        // fused: the generator writes the root pre-pass rows the decode
+        // kernel reads (fast engine in pre-mode; symbols < q <= v need no
+        // range check); else int32 symbols in a buffer of its own
+        const bool fused = d->engine == QPD_ENGINE_FAST && d->pre && ch->q <= d->v;
+        int64_t chunk;
+        if (fused) {
+            int r0 = QPD_OK;
+            chunk = ensure_pre_rows(d, std::min<int64_t>(B, d->pre_chunk), &r0);
+            if (r0) return r0;
+        } else {
+            chunk = std::min<int64_t>(B, (int64_t)1 << 20);
+            if (d->mc_sym_cap < chunk) {
+                if (d->mc_sym.p) QPD_HIP(hipFree(d->mc_sym.p));
+                d->mc_sym.p = nullptr;
+                d->mc_sym_cap = 0;
+                QPD_HIP(hipMalloc(&d->mc_sym.p, (size_t)chunk * d->N * sizeof(int32_t)));
+                d->mc_sym_cap = chunk;
             }
-            int rc2 = upload(d->mc_pref, pref.data(), pref.size(), d->hs);
-            if (rc2) return rc2;
-            rc2 = upload(d->mc_crc, tab.data(), tab.size(), d->hs);
-            if (rc2) return rc2;
         }
-        qpd::McChannel C;
-        std::memset(&C, 0, sizeof(C));
-        C.N = d->N;
-        C.K = d->K;
-        C.A = d->crc_n > 0 ? d->ca_A : d->K;
-        C.crc_n = d->crc_n;
-        C.q = ch->q;
-        C.n_edges = ch->n_edges;
-        C.seed_lo = (uint32_t)seed;
-        C.seed_hi = (uint32_t)(seed >> 32);
-        C.sigma = ch->sigma;
-        C.s2 = ch->sigma * ch->sigma;
-        C.info_mask = (const uint32_t *)d->info_mask.p;
-        C.info_pref = (const int32_t *)d->mc_pref.p;
-        C.crc_tab = (const uint32_t *)d->mc_crc.p;
-        for (int i = 0; i < ch->n_edges; ++i) C.edges[i] = ch->edges[i];
-        for (int i = 0; i + 1 < ch->n_edges; ++i) C.lut[i] = ch->lut[i];
-        int dev = 0, ncu = 256;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        const int grid = (int)std::min<int64_t>(B, (int64_t)ncu * 32);
-        const size_t lds = qpd::mc_lds_bytes(d->N, d->K);
-        return timed_launch(d, QPD_KC_MC, st, [&]() -> int {
-            hipLaunchKernelGGL(qpd::mc_frames_kernel, dim3(grid), dim3(64), lds, st, C, frame0, B, d_msg, d_symbols);
-            QPD_HIP(hipGetLastError());
-            return QPD_OK;
-        });
+        DeviceBuf &buf = fused ? d->pre_buf : d->mc_sym;
+        for (int64_t f0 = 0; f0 < B; f0 += chunk) {
+            const int64_t Bc = std::min<int64_t>(chunk, B - f0);
+            int r = mc_launch(d, ch, seed, frame0 + f0, Bc, d_msg + f0 * d->out_bits, (int32_t *)buf.p, fused, st);
+            if (r) return r;
+            uint8_t *out = d_out + f0 * d->out_bits;
+            r = fused ? decode_pre_rows(d, (const uint32_t *)buf.p, Bc, out, st)
+                      : decode_impl(d, (const int32_t *)buf.p, Bc, out, st);
+            if (r) return r;
+        }
+        return QPD_OK;
     });
 }
 
@@ -1434,15 +1530,6 @@ int qpd_debug_stamps(unsigned long long *out64) {
     QPD_HIP(hipMemcpyFromSymbol(out64, HIP_SYMBOL(qpd::qpd_stamp_acc), 64 * sizeof(unsigned long long)));
     static const unsigned long long zero[64] = {0};
     QPD_HIP(hipMemcpyToSymbol(HIP_SYMBOL(qpd::qpd_stamp_acc), zero, sizeof(zero)));
-    return QPD_OK;
-}
-#endif
-#ifdef QPD_STAMPS_SEL
-int qpd_debug_sel_stats(unsigned long long *out64) {
-    QPD_HIP(hipDeviceSynchronize());
-    QPD_HIP(hipMemcpyFromSymbol(out64, HIP_SYMBOL(qpd::qpd_sel_stats), 64 * sizeof(unsigned long long)));
-    static const unsigned long long zero[64] = {0};
-    QPD_HIP(hipMemcpyToSymbol(HIP_SYMBOL(qpd::qpd_sel_stats), zero, sizeof(zero)));
     return QPD_OK;
 }
 #endif

@@ -5,23 +5,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "qpd_types.hpp"
+
 namespace qpd {
-
-enum OpType : int32_t {
-    OP_F = 0,       // left child symbols  (f LUT), depth d -> d+1
-    OP_G = 1,       // right child symbols (g LUT), depth d -> d+1
-    OP_LEAF_L = 2,  // left leaf 2*node of a depth n-1 node (f LUT at j=0)
-    OP_LEAF_R = 3,  // right leaf 2*node+1                  (g LUT at j=0)
-    OP_COMB = 4,    // partial-sum combine u(), utils.cpp:62-67
-    OP_R0 = 5,
-    OP_R1 = 6,
-    OP_REP = 7,
-    OP_SPC = 8
-};
-
-struct Op {
-    int32_t type, d, node, aux;  // aux: frozen flag for leaves
-};
 
 // Task queue of the persistent decode kernels.
 #ifndef QPD_DYN
@@ -32,7 +18,7 @@ struct Op {
 // relative to the launch's base.  The counter is never reset: a launch of T
 // tasks on a grid of G <= T waves takes exactly T values (T - G successful
 // takes, then one failed take per wave), so the host advances the base by T
-// per launch (qpd_capi.hip: next_base) and the next launch on the decoder
+// per launch (qpd_capi.hip: qpd_decoder::task_base) and the next launch on the decoder
 // starts where this one ended.  uint32 arithmetic: wrap-around is harmless.
 // Launches on one decoder are ordered by the host (stream events), so no
 // launch ever sees another's takes.
@@ -41,24 +27,6 @@ __device__ __forceinline__ int64_t wave_take(uint32_t *ctr, uint32_t base) {
     if (threadIdx.x == 0) v = atomicAdd(ctr, 1u);
     return (int64_t)(uint32_t)(__builtin_amdgcn_readfirstlane(v) - base);
 }
-
-constexpr int kMaxDepth = 16;  // N <= 65536
-constexpr int kMaxL = 8;       // fast engine: 2L <= 16, libstdc++ sorts by insertion (stable)
-constexpr int kMaxM = kMaxL - 1;
-constexpr int kMaxLWide = 32;  // generic engine: 2L <= 64, libstdc++ introsort replayed (stl_sort.hpp)
-
-// Decoder families of the kernels (the float-domain decoders use the same
-// family ids with a DOM_* symbol domain; K_SC_FLOAT is the C-ABI's kind 0).
-enum Kind : int32_t { K_SC_FLOAT = 0, K_SC_LUT = 1, K_SCL_LUT = 2, K_FASTSC_LUT = 3, K_FASTSCL_LUT = 4 };
-
-// Symbol domains of the generic engine: LUT symbols (int, f/g by tables) or
-// fp64 LLRs (min-sum f/g), optionally re-quantized after every f/g.
-enum Dom : int32_t { DOM_LUT = 0, DOM_FLOAT = 1, DOM_UNIFORM = 2, DOM_LLOYD = 3 };
-
-// Device error flags (DevPlan/FastPlan err word).
-enum ErrFlag : int32_t { ERR_SYMBOL = 1, ERR_LLOYD = 2, ERR_NAN_PM = 4 };
-
-
 
 // ---------------------------------------------------------------------------
 // small helpers
@@ -148,9 +116,6 @@ __device__ __forceinline__ void rank8_partner(uint64_t K, uint64_t F, uint64_t F
 
 // Generic form: any L <= 8 (lane groups of G = pow2 >= L), `sel` = 64 ints.
 __device__ __forceinline__ Sel select_survivors(double kk, double kf, int gl, int gbase, int L, int *sel) {
-#ifdef QPD_EXP_NOSEL  // timing experiment only: wrong results
-    if (L > 0) return Sel{gl, false};
-#endif
     int rk = 0, rf = 0;
     for (int j = 0; j < L; ++j) {
         const double ok = shfld(kk, gbase + j);
@@ -180,9 +145,6 @@ __device__ __forceinline__ Sel select_survivors(double kk, double kf, int gl, in
 // scatter (ranks >= 8 go to a per-lane junk slot), so several independent
 // selections can interleave in one basic block.  `sel` = 128 ints.
 __device__ __forceinline__ Sel select_survivors8(double kk, double kf, int gl, int gbase, int lane, int *sel) {
-#ifdef QPD_EXP_NOSEL
-    return Sel{gl, false};
-#endif
     const uint64_t K = __builtin_bit_cast(uint64_t, kk), F = __builtin_bit_cast(uint64_t, kf);
     const uint64_t hk = dpp64<kDppHalfMirror>(K), hf = dpp64<kDppHalfMirror>(F);
     const uint64_t F1 = F + 1;

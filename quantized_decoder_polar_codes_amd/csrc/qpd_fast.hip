@@ -438,9 +438,6 @@ struct Path {
     uint64_t ps, pu;
 };
 
-#ifdef QPD_STAMPS_SEL
-__device__ unsigned long long qpd_sel_stats[64];
-#endif
 constexpr int kSelInts = 128;  // per set: 64 slots + 64 junk slots (select_survivors8)
 
 // max of two non-negative doubles given as bits (one v_max_f64).
@@ -450,82 +447,35 @@ __device__ __forceinline__ uint64_t dmax_bits(uint64_t a, uint64_t b) {
     return __builtin_bit_cast(uint64_t, r);
 }
 
+// Identity test of the L = 8 survivor selection, for every lane group of the
+// wave at once: the keeps K_j (this lane's keep key) are already in stable
+// order (K_0 <= ... <= K_7) and no flip F_j beats the largest keep (a flip
+// equal to a keep loses the tie: its candidate index is higher).  The stable
+// sort of the 16 candidates then puts keep_j in slot j -- nothing moves and
+// no flip survives.  Keys are >= +0 or +inf, never NaN (a NaN metric raises
+// ERR_NAN_PM in the generic engine; LUT quanta are finite): max over doubles =
+// max over their bits.  v_max_f64 by inline asm: the builtin would
+// canonicalize the DPP operands first (two more VALU per step).
+__device__ __forceinline__ bool keep_all8(uint64_t K, uint64_t F, int gl) {
+    uint64_t mk = K;
+    mk = dmax_bits(mk, dpp64<kDppXor1>(mk));
+    mk = dmax_bits(mk, dpp64<kDppXor2>(mk));
+    mk = dmax_bits(mk, dpp64<kDppHalfMirror>(mk));  // lane i^7 lies in the other quad
+    const uint64_t Kn = dpp64<kDppRowShl1>(K);       // keep of slot gl+1
+    return __ballot(F >= mk && (gl == 7 || K <= Kn)) == ~0ull;
+}
+
 // Info leaf with quanta dm: keep the L best of {keep, flip} candidates.
 // Returns the new decision; `extra` words follow the surviving lineage.
 template <bool L8, int NX>
 __device__ __forceinline__ uint32_t leaf_fork(Path &st, double dm, int gl, int gbase, int L, int lane, int *sel,
                                               uint32_t (&extra)[NX]) {
     const double kf = st.pm + fabs(dm);
-#ifdef QPD_STAMPS_SEL
-    if (L8) {  // diagnostic: how often would a keep-all / identity fast path apply?
-        uint64_t K = __builtin_bit_cast(uint64_t, st.pm), F = __builtin_bit_cast(uint64_t, kf);
-        uint64_t mxk = K, mnf = F;
-        for (int m = 1; m < 8; m <<= 1) {
-            const uint64_t ok = shfl64(mxk, lane ^ m), of = shfl64(mnf, lane ^ m);
-            mxk = ok > mxk ? ok : mxk;
-            mnf = of < mnf ? of : mnf;
-        }
-        const uint64_t Kn = shfl64(K, (lane & 7) == 7 ? lane : lane + 1);
-        const bool srt = K <= Kn;
-        const bool ka = mxk <= mnf;
-        const uint64_t bka = __ballot(ka), bid = __ballot(ka && srt);
-        const uint64_t bsrt = __ballot(srt);
-        if (lane == 0) {
-            unsigned long long *c = qpd_sel_stats + 8 * (blockIdx.x & 7);
-            atomicAdd(c + 0, 1ull);
-            atomicAdd(c + 1, (unsigned long long)(bka == ~0ull));
-            atomicAdd(c + 2, (unsigned long long)(bid == ~0ull));
-            atomicAdd(c + 3, (unsigned long long)__popcll(bka) / 8);
-            atomicAdd(c + 4, (unsigned long long)__popcll(bka & bsrt));
-        }
-    }
-#endif
     const uint32_t hd = dm < 0;  // H4: SCL family `< 0`
-#ifndef QPD_NO_FASTKEEP
-    if constexpr (L8) {
-        // Fast path, taken when it holds for every group of the wave (about
-        // 2/3 of the info leaves on the bench channel): the keeps are already
-        // in stable order (pm_0 <= ... <= pm_7) and no flip beats any keep
-        // (max pm <= every kf).  The stable sort of the 16 candidates then
-        // puts keep_j in slot j: nothing moves, the decision is the hard one.
-        // Path metrics are >= +0 or +inf, never NaN (a NaN metric raises ERR_NAN_PM in
-        // the generic engine; LUT quanta are finite): max over doubles = max over
-        // their bits.  v_max_f64 by inline asm: the builtin would canonicalize the
-        // DPP results first (two more VALU per step).
-        const uint64_t K = __builtin_bit_cast(uint64_t, st.pm), F = __builtin_bit_cast(uint64_t, kf);
-#ifdef QPD_FAST_HI
-        // Conservative 32-bit form: hi(F) > max hi(K) implies F > every keep;
-        // an undecided case (equal high words: +inf or |dm| below 2^-20 of pm)
-        // takes the full selection, which is always exact.
-        const uint32_t kh = (uint32_t)(K >> 32), fh = (uint32_t)(F >> 32);
-        uint32_t mh = kh;
-        mh = max(mh, (uint32_t)__builtin_amdgcn_mov_dpp((int)mh, kDppXor1, 0xF, 0xF, true));
-        mh = max(mh, (uint32_t)__builtin_amdgcn_mov_dpp((int)mh, kDppXor2, 0xF, 0xF, true));
-        mh = max(mh, (uint32_t)__builtin_amdgcn_mov_dpp((int)mh, kDppHalfMirror, 0xF, 0xF, true));
-        const uint64_t Kn = dpp64<kDppRowShl1>(K);  // pm of slot gl+1
-        // lane masks straight from the compares (no ballot materialization)
-        const uint64_t okm = __builtin_amdgcn_uicmp(fh, mh, 34 /* ugt */) &
-                             (__builtin_amdgcn_uicmp((uint32_t)gl, 7u, 32 /* eq */) |
-                              __builtin_amdgcn_uicmpl(K, Kn, 37 /* ule */));
-        if (okm == ~0ull) return hd;
-#else
-        uint64_t mk = K;
-        mk = dmax_bits(mk, dpp64<kDppXor1>(mk));
-        mk = dmax_bits(mk, dpp64<kDppXor2>(mk));
-        mk = dmax_bits(mk, dpp64<kDppHalfMirror>(mk));  // lane i^7 lies in the other quad
-        const uint64_t Kn = dpp64<kDppRowShl1>(K);  // pm of slot gl+1
-#ifdef QPD_FAST_MASK
-        const uint64_t okm = __builtin_amdgcn_uicmpl(F, mk, 35 /* uge */) &
-                             (__builtin_amdgcn_uicmp((uint32_t)gl, 7u, 32 /* eq */) |
-                              __builtin_amdgcn_uicmpl(K, Kn, 37 /* ule */));
-        if (okm == ~0ull) return hd;
-#else
-        const bool ok = F >= mk && (gl == 7 || K <= Kn);
-        if (__ballot(ok) == ~0ull) return hd;
-#endif
-#endif
-    }
-#endif
+    // Fast path (about 2/3 of the info leaves on the bench channel): the
+    // selection is the identity, the decision the hard one.
+    if constexpr (L8)
+        if (keep_all8(__builtin_bit_cast(uint64_t, st.pm), __builtin_bit_cast(uint64_t, kf), gl)) return hd;
     const Sel sl = L8 ? select_survivors8(st.pm, kf, gl, gbase, lane, sel) : select_survivors(st.pm, kf, gl, gbase, L, sel);
     const int p = gbase + sl.parent;
     const uint32_t dec = (uint32_t)__shfl((int)hd, p) ^ (sl.upper ? 1u : 0u);
@@ -557,49 +507,6 @@ __device__ __forceinline__ void leaf_decide(Path (&st)[NS], const double (&dm)[N
         }
         return;
     }
-#if defined(QPD_ILV) && !defined(QPD_NO_FASTKEEP)
-    if constexpr (L8 && NS > 1) {
-        // All sets in one straight-line block: the identity checks of every set,
-        // one wave-uniform branch, then (if any set needs it) the selections and
-        // fork shuffles of every set interleaved.  Forking set by set behind a
-        // branch each would serialize the sets' dependency chains.  A set whose
-        // identity check holds gets the identity from the full selection too.
-        double kf[NS];
-        uint32_t hd[NS];
-        bool fast = true;
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            kf[s] = st[s].pm + fabs(dm[s]);
-            hd[s] = dm[s] < 0;  // H4: SCL family `< 0`
-            const uint64_t K = __builtin_bit_cast(uint64_t, st[s].pm), F = __builtin_bit_cast(uint64_t, kf[s]);
-            uint64_t mk = K;
-            mk = dmax_bits(mk, dpp64<kDppXor1>(mk));
-            mk = dmax_bits(mk, dpp64<kDppXor2>(mk));
-            mk = dmax_bits(mk, dpp64<kDppHalfMirror>(mk));
-            const uint64_t Kn = dpp64<kDppRowShl1>(K);
-            fast = fast && __ballot(F >= mk && (gl == 7 || K <= Kn)) == ~0ull;
-        }
-        if (fast) {
-#pragma unroll
-            for (int s = 0; s < NS; ++s) dec[s] = hd[s];
-            return;
-        }
-        Sel sl[NS];
-#pragma unroll
-        for (int s = 0; s < NS; ++s) sl[s] = select_survivors8(st[s].pm, kf[s], gl, gbase, lane, sel + sstride * s);
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            const int p = gbase + sl[s].parent;
-            dec[s] = (uint32_t)__shfl((int)hd[s], p) ^ (sl[s].upper ? 1u : 0u);
-            st[s].pm = pick(sl[s].upper, shfld(kf[s], p), shfld(st[s].pm, p));
-            st[s].ps = shfl64(st[s].ps, p);
-            st[s].pu = shfl64(st[s].pu, p);
-#pragma unroll
-            for (int i = 0; i < NX; ++i) extra[s][i] = (uint32_t)__shfl((int)extra[s][i], p);
-        }
-        return;
-    }
-#endif
 #pragma unroll
     for (int s = 0; s < NS; ++s) dec[s] = leaf_fork<L8>(st[s], dm[s], gl, gbase, L, lane, sel + sstride * s, extra[s]);
 }
@@ -626,44 +533,6 @@ __device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], u
                                          uint32_t (&c)[NS]) {
     double dm[NS];
     uint32_t bl[NS], br[NS];
-#ifdef QPD_SPEC_R
-    if (kList && !(fr & 1)) {
-        // Info left leaf: the right leaf's quanta for both of its possible
-        // left decisions are looked up before the fork (they depend only on the
-        // lineage's W1), follow the surviving lineage through the fork, and
-        // the decision then selects one -- the right leaf's two dependent LDS
-        // lookups leave the fork-to-fork critical path.
-        uint32_t xx[NS][6];
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            const uint32_t a = (x[s][1] >> 16) & 15u, b = (x[s][1] >> 20) & 15u, ab = (a << 4) | b;
-            dm[s] = shfld(V, vo + (int)lut4(Tf, ab + fo));
-            const double r0 = shfld(V, vo + 16 + (int)lut4(Tg, ab)), r1 = shfld(V, vo + 16 + (int)lut4(Tg, 256u | ab));
-            const uint64_t b0 = __builtin_bit_cast(uint64_t, r0), b1 = __builtin_bit_cast(uint64_t, r1);
-            xx[s][0] = x[s][0];
-            xx[s][1] = x[s][1];
-            xx[s][2] = (uint32_t)b0;
-            xx[s][3] = (uint32_t)(b0 >> 32);
-            xx[s][4] = (uint32_t)b1;
-            xx[s][5] = (uint32_t)(b1 >> 32);
-        }
-        leaf_decide<kList, L8>(st, dm, false, gl, gbase, L, lane, sel, sstride, xx, bl);
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            x[s][0] = xx[s][0];
-            x[s][1] = (xx[s][1] & ~(1u << 24)) | (bl[s] << 24);
-            const uint64_t r = bl[s] ? ((uint64_t)xx[s][5] << 32 | xx[s][4]) : ((uint64_t)xx[s][3] << 32 | xx[s][2]);
-            dm[s] = __builtin_bit_cast(double, r);
-        }
-        leaf_decide<kList, L8>(st, dm, fr & 2, gl, gbase, L, lane, sel, sstride, x, br);
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            const uint32_t bl2 = (x[s][1] >> 24) & 1u;
-            c[s] = (bl2 ^ br[s]) | (br[s] << 1);
-        }
-        return;
-    }
-#endif
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const uint32_t a = (x[s][1] >> 16) & 15u, b = (x[s][1] >> 20) & 15u;
@@ -805,6 +674,13 @@ __device__ __forceinline__ uint32_t r1_layers(Path &st, int *sel, int gl, int gb
             const uint32_t sym = __builtin_amdgcn_ubfe(symp, 4 * layer, 4);
             const double own_ms = fabs(uni ? shfld(vrow, (int)sym) : vq[(size_t)own * v + sym]);
             const double kf = st.pm + shfld(own_ms, o);
+            // Identity selection in every group: no flip survives and no
+            // lineage moves, and since each slot's magnitudes ascend with the
+            // layer (argsort order) and pm + a is monotone in a, every later
+            // layer's flips are at least as large -- all remaining layers are
+            // the identity too, so the node is decided.
+            if constexpr (L8)
+                if (keep_all8(__builtin_bit_cast(uint64_t, st.pm), __builtin_bit_cast(uint64_t, kf), gl)) break;
             const int pos_old = __shfl(own, o);  // H2
             const Sel sl = L8 ? select_survivors8(st.pm, kf, gl, gbase, lane, sel)
                               : select_survivors(st.pm, kf, gl, gbase, L, sel);
@@ -990,8 +866,15 @@ __device__ __forceinline__ void r1_large(const FastPlan &P, const Mem &M, const 
 // without LDS room; N >= 2048 codes).  Only those plans get it compiled in:
 // its argsort stack and arrays cost the other instantiations registers and
 // scratch (+3 % FastSCL-LUT at N = 1024 without it).
+// QPD_SPECIAL_NOINLINE (A/B builds): special nodes as a called function, so
+// that their register needs do not shape the main loop's allocation.
+#ifdef QPD_SPECIAL_NOINLINE
+#define QPD_SPECIAL_ATTR __attribute__((noinline))
+#else
+#define QPD_SPECIAL_ATTR __forceinline__
+#endif
 template <bool kList, bool L8, bool R1L>
-__device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, const MOp &op, Path &st, int *sel, int gl,
+__device__ QPD_SPECIAL_ATTR void special_op(const FastPlan &P, const Mem &M, const MOp &op, Path &st, int *sel, int gl,
                                            int gbase, int L, int lane) {
     const int fl = op.flags;
     const int temp = op.cnt;
@@ -1054,12 +937,16 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
                         kf += l[i] >= 0 ? fabs(l[i]) : 0.0;
                     }
             }
-            const Sel sx = L8 ? select_survivors8(kk, kf, gl, gbase, lane, sel) : select_survivors(kk, kf, gl, gbase, L, sel);
-            const int p = gbase + sx.parent;
-            st.pm = pick(sx.upper, shfld(kf, p), shfld(kk, p));
-            st.ps = shfl64(st.ps, p);
-            st.pu = shfl64(st.pu, p);
-            fill = sx.upper ? 0xffffffffu : 0u;
+            if (L8 && keep_all8(__builtin_bit_cast(uint64_t, kk), __builtin_bit_cast(uint64_t, kf), gl)) {
+                st.pm = kk;  // identity selection: every path keeps its all-zeros codeword
+            } else {
+                const Sel sx = L8 ? select_survivors8(kk, kf, gl, gbase, lane, sel) : select_survivors(kk, kf, gl, gbase, L, sel);
+                const int p = gbase + sx.parent;
+                st.pm = pick(sx.upper, shfld(kf, p), shfld(kk, p));
+                st.ps = shfl64(st.ps, p);
+                st.pu = shfl64(st.pu, p);
+                fill = sx.upper ? 0xffffffffu : 0u;
+            }
         }
         const uint32_t m = temp < 32 ? ((1u << temp) - 1u) : 0xffffffffu;
         for (int w = 0; w < nwo; ++w) M.st(dl, op.dst_row + w, lane, fill & m);

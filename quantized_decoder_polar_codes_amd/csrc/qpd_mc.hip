@@ -20,6 +20,11 @@
 // the first edge >= llr whatever the guess (uniform edges, the driver's
 // linspace, need 0-1 steps).
 //
+// PRE mode (qpd_mc_decode): the frame's symbols are staged in LDS and the
+// kernel writes the decoder's root pre-pass row instead (root_pre_kernel,
+// qpd_fast.hip), so generation feeds the decode kernel directly: no int32
+// symbols (4 KB per frame at N = 1024) written to HBM and read back.
+//
 // Work mapping: one wave per frame (grid-stride).  The frame's bits are
 // handled bit-packed (32 positions per dword): lane d draws message dword d,
 // the CRC is a table XOR (the register is linear in the message bits), the
@@ -72,6 +77,11 @@ struct McChannel {
     const uint32_t *crc_tab;    // [A] CRC register contribution of message bit j (CA kinds)
     double edges[kMcMaxEdges];  // [n_edges], ascending (kernel arguments; staged in LDS)
     int32_t lut[kMcMaxEdges - 1];
+    // PRE mode (qpd_mc_decode on a fast-engine decoder in pre-mode): instead
+    // of int32 symbols, each frame's root pre-pass row (root_pre_kernel's
+    // layout: f(y), g(y, 0), g(y, 1) as nibble words, N/4 dwords per frame),
+    // computed from the frame's symbols staged in LDS with the root's tables.
+    const uint32_t *f_tab, *g_tab;  // node 0's nibble tables (FastPlan f_tab / g_tab)
 };
 
 // 53-bit uniform from two Philox words: k = (a >> 5) * 2^26 + (b >> 6), k * 2^-53.
@@ -107,10 +117,17 @@ __device__ inline void mc_sincos(double x, double *sn, double *cs) {
     }
 }
 
+template <bool PRE>
 __global__ __launch_bounds__(64) void mc_frames_kernel(McChannel C, int64_t frame0, int64_t B,
                                                        uint8_t *__restrict__ msg_out, int32_t *__restrict__ sym_out) {
 #pragma clang fp contract(off)
     extern __shared__ uint32_t lds_mc[];
+    // PRE: sym_out holds pre-pass rows (N/4 dwords per frame), see McChannel
+    uint32_t Tf = 0, Tg = 0;
+    if (PRE) {
+        Tf = C.f_tab[threadIdx.x & 31];
+        Tg = C.g_tab[threadIdx.x];
+    }
     const int t = threadIdx.x;
     const int N = C.N, K = C.K, A = C.A, M = C.n_edges - 1;
     const int nw = (N + 31) >> 5;        // u / x words
@@ -119,6 +136,7 @@ __global__ __launch_bounds__(64) void mc_frames_kernel(McChannel C, int64_t fram
     int32_t *lut = reinterpret_cast<int32_t *>(edges + kMcMaxEdges);
     uint32_t *xw = reinterpret_cast<uint32_t *>(lut + kMcMaxEdges);
     uint32_t *bw = xw + nw;               // message + CRC bits (kw + 2 words)
+    uint8_t *sy = reinterpret_cast<uint8_t *>(bw + kw + 2);  // PRE: the frame's N channel symbols
     for (int i = t; i < C.n_edges; i += 64) edges[i] = C.edges[i];
     for (int i = t; i < M; i += 64) lut[i] = C.lut[i];
     const double lo_edge = C.edges[0], hi_edge = C.edges[M];
@@ -215,15 +233,44 @@ __global__ __launch_bounds__(64) void mc_frames_kernel(McChannel C, int64_t fram
                     s_out[h] = lut[lo - 1];
                 }
             }
-            *reinterpret_cast<int2 *>(sym_out + f * N + 2 * p) = make_int2(s_out[0], s_out[1]);
+            if (PRE)
+                *reinterpret_cast<uint16_t *>(sy + 2 * p) = (uint16_t)(s_out[0] | (s_out[1] << 8));
+            else
+                *reinterpret_cast<int2 *>(sym_out + f * N + 2 * p) = make_int2(s_out[0], s_out[1]);
         }
         __syncthreads();
+        if (PRE) {
+            // root_pre_kernel's row from the staged symbols: word w of f(y),
+            // g(y, 0), g(y, 1) from symbols [8w, 8w+8) and [N/2 + 8w, ...);
+            // whole waves stay active through the lookups (inactive lanes
+            // would read 0 from the table registers)
+            const int nwh = N >> 4;  // words per segment (N >= 16)
+            uint32_t *row = reinterpret_cast<uint32_t *>(sym_out) + f * (N >> 2);
+            for (int w0 = 0; w0 < nwh; w0 += 64) {
+                const int w = min(w0 + t, nwh - 1);
+                uint32_t a = 0, b = 0;
+                for (int i = 0; i < 8; ++i) {
+                    a |= (uint32_t)sy[8 * w + i] << (4 * i);
+                    b |= (uint32_t)sy[(N >> 1) + 8 * w + i] << (4 * i);
+                }
+                const uint32_t fw = lut_vec<8>(Tf, a, b, 0u);
+                const uint32_t g0 = lut_vec<8>(Tg, a, b, 0u);
+                const uint32_t g1 = lut_vec<8>(Tg, a, b, 0xFFu);
+                if (w0 + t < nwh) {
+                    row[w] = fw;
+                    row[nwh + w] = g0;
+                    row[2 * nwh + w] = g1;
+                }
+            }
+            __syncthreads();
+        }
     }
 }
 
 // Dynamic LDS of mc_frames_kernel.
-inline size_t mc_lds_bytes(int N, int K) {
-    return kMcMaxEdges * (sizeof(double) + sizeof(int32_t)) + 4 * (((N + 31) >> 5) + ((K + 31) >> 5) + 2);
+inline size_t mc_lds_bytes(int N, int K, bool pre) {
+    return kMcMaxEdges * (sizeof(double) + sizeof(int32_t)) + 4 * (((N + 31) >> 5) + ((K + 31) >> 5) + 2) +
+           (pre ? (size_t)N : 0);
 }
 
 }  // namespace qpd

@@ -9,8 +9,11 @@ py_FastSCDecoder.cpp:11-14, py_FastSCLDecoder.cpp:10-13,
 py_SCUniformDecoder.cpp:10-14, py_SCLUniformQuantizedDecoder.cpp:10-14,
 py_SCLloydQuantizedDecoder.cpp:10-15, py_SCLLloydQuantizedDecoder.cpp:10-15):
 ``decode`` takes one frame and returns a new ``numpy.ndarray`` of dtype uint8
-and length K (A for the CRC-aided classes).  Every decode runs on the GPU
-through libqpd.so; there is no CPU path.
+and length K (A for the CRC-aided classes).  Every decode runs in libqpd.so:
+batches on the GPU kernels, the few frames of a per-frame call on its host
+engine (qpd_decode_host; a GPU call costs ~0.1 ms before decoding anything,
+the reference's SC-LUT call ~10 us).  The package fails to load without the
+library and a decoder cannot be created without a HIP device.
 
 Additions (not in the reference): ``decode_batch(x[B, N])`` for throughput
 (numpy in -> numpy out; a torch CUDA tensor in -> torch CUDA tensor out,
@@ -20,6 +23,7 @@ where the reference has undefined behaviour.
 from __future__ import annotations
 
 import ctypes
+import threading
 
 import numpy as np
 
@@ -64,7 +68,7 @@ class _DecoderBase:
 
     def __init__(self, N, K, L, frozen_bits, message_bits, node_type, packed: PackedLUT | None, device=None,
                  max_waves: int = 0, engine: str = "auto", A: int | None = None, crc_n: int = 24,
-                 crc_loc=CRC24_LOC, quant: UniformQuant | LloydQuant | None = None):
+                 crc_loc=CRC24_LOC, quant: UniformQuant | LloydQuant | None = None, create: bool = True):
         self.N = int(N)
         self.K = int(K)
         self.L = int(L)
@@ -80,7 +84,6 @@ class _DecoderBase:
         if self.node_type is not None and self.node_type.size != 2 * self.N - 1:
             raise ValueError(f"node_type must have 2N-1={2 * self.N - 1} entries, got {self.node_type.size}")
         self.packed = packed
-        lib = _lib.load()
         cfg = _lib.QpdConfig()
         cfg.kind = self._kind
         cfg.N, cfg.K, cfg.L = self.N, self.K, self.L
@@ -117,9 +120,22 @@ class _DecoderBase:
         if self._kind in (_lib.QPD_CASCL_LUT, _lib.QPD_CAFASTSCL_LUT, _lib.QPD_CASCL_FLOAT):
             cfg.A, cfg.crc_n = self.A, int(crc_n)
             cfg.crc_loc, cfg.crc_loc_count = _ptr(self._crc_loc), self._crc_loc.size
+        self._cfg = cfg  # the arrays it points to are attributes of self
+        if not create:  # configuration only (tests of the host engine on CPU): no device decoder
+            self._h = None
+            return
         h = ctypes.c_void_p()
+        lib = _lib.load()
         _lib.check(lib.qpd_create(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
+        # the per-frame call's own buffers and bound entry point (numpy's
+        # pointer extraction costs ~2 us per array, as much as a whole SC-LUT
+        # frame on the host engine): decode() copies into / out of them
+        self._one_in = np.empty(self.N, dtype=np.float64 if self._float_input else np.int32)
+        self._one_out = np.empty(self.out_bits, dtype=np.uint8)
+        self._one_args = (ctypes.c_void_p(self._one_in.ctypes.data), ctypes.c_void_p(self._one_out.ctypes.data))
+        self._one_fn = lib.qpd_decode_f64_host if self._float_input else lib.qpd_decode_host
+        self._one_lock = threading.Lock()
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -150,14 +166,6 @@ class _DecoderBase:
         return {name: (ms[i], n[i]) for i, name in enumerate(("pre", "decode", "mc"))}
 
     # -- decoding --------------------------------------------------------------
-    def _frame(self, x) -> np.ndarray:
-        a = np.asarray(x)
-        a = a.astype(np.float64 if self._float_input else np.int32).reshape(-1)
-        if a.size < self.N:
-            raise ValueError(f"decode expects N={self.N} values, got {a.size}")
-        # the reference reads the first N values of the buffer (shape (N,) or (1, N))
-        return np.ascontiguousarray(a[: self.N])
-
     def decode_batch(self, x):
         """Decode B frames.  numpy [B, N] -> numpy uint8 [B, K] (synchronous);
         torch CUDA tensor [B, N] -> torch CUDA uint8 [B, K] on the current stream.
@@ -184,8 +192,24 @@ class _DecoderBase:
         _lib.check(fn(self._h, _ptr(a), B, _ptr(out)))
         return out
 
+    def set_host_engine(self, mode: str = "auto") -> None:
+        """Where host-buffer calls (``decode``, numpy ``decode_batch``) run:
+        "auto" (the host engine for the few frames a per-frame call brings, the
+        GPU for batches; ``info()["host_max_frames"]``), "gpu" or "cpu"."""
+        m = {"auto": _lib.QPD_HOST_AUTO, "gpu": _lib.QPD_HOST_GPU, "cpu": _lib.QPD_HOST_CPU}[mode]
+        _lib.check(_lib.load().qpd_set_host_engine(self._h, m))
+
     def _decode_one(self, x) -> np.ndarray:
-        return self.decode_batch(self._frame(x)[None])[0].copy()
+        # the per-frame call (mainQuantizedDecoder_LLRDomain.py:178): one frame
+        # straight to the host-buffer entry point, no batch reshaping; the
+        # values are force-cast as pybind11's array_t<int> / <double> does
+        a = np.asarray(x).reshape(-1)
+        if a.size < self.N:
+            raise ValueError(f"decode expects N={self.N} values, got {a.size}")
+        with self._one_lock:  # the GIL is released during the call: keep the buffers per call
+            np.copyto(self._one_in, a[: self.N], casting="unsafe")
+            _lib.check(self._one_fn(self._h, self._one_args[0], 1, self._one_args[1]))
+            return self._one_out.copy()
 
 
 class _LUTDecoder(_DecoderBase):

@@ -74,6 +74,19 @@ class GpuFrames:
         self.seed = int(seed)
         self.device = torch.device("cuda", decoder.device if decoder.device >= 0 else torch.cuda.current_device())
 
+    def decode_frames(self, frame0: int, B: int):
+        """(msg, decoded bits) of frames [frame0, frame0+B): the same bits as
+        decode_batch(self(frame0, B)[1]), by qpd_mc_decode (generation feeds the
+        decode kernel's pre-pass rows directly, no int32 symbols)."""
+        torch = self.torch
+        msg = torch.empty((B, self.dec.out_bits), dtype=torch.uint8, device=self.device)
+        bits = torch.empty((B, self.dec.out_bits), dtype=torch.uint8, device=self.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        _lib.check(_lib.load().qpd_mc_decode(self.dec._h, ctypes.byref(self.ch), ctypes.c_uint64(self.seed), frame0, B,
+                                             ctypes.c_void_p(msg.data_ptr()), ctypes.c_void_p(bits.data_ptr()),
+                                             ctypes.c_void_p(stream)))
+        return msg, bits
+
     def __call__(self, frame0: int, B: int):
         torch = self.torch
         msg = torch.empty((B, self.dec.out_bits), dtype=torch.uint8, device=self.device)
@@ -97,7 +110,19 @@ def _frame_errors(bits, msg):
     return (np.asarray(bits) != np.asarray(msg)).sum(axis=1).astype(np.int64)
 
 
-def _run_point_all(generate, decode, K, ebn0_db, batch, max_blocks, world, rank, group, count_device):
+def _step_fn(generate, decode, gen_decode):
+    """(msg, bits) of a frame range: one fused call, or generate then decode."""
+    if gen_decode is not None:
+        return gen_decode
+
+    def step(lo, n):
+        msg, sym = generate(lo, n)
+        return msg, decode(sym)
+
+    return step
+
+
+def _run_point_all(step_fn, K, ebn0_db, batch, max_blocks, world, rank, group, count_device):
     """run_point without early stop (the driver's MaxBlock branch, :194-196):
     counters accumulate on the device, one all-reduce at the end."""
     import torch
@@ -110,8 +135,8 @@ def _run_point_all(generate, decode, K, ebn0_db, batch, max_blocks, world, rank,
         lo = f0 + min(rank * batch, step)
         hi = f0 + min((rank + 1) * batch, step)
         if hi > lo:
-            msg, sym = generate(lo, hi - lo)
-            e = _frame_errors(decode(sym), msg)
+            msg, bits = step_fn(lo, hi - lo)
+            e = _frame_errors(bits, msg)
             e_t = (e if isinstance(e, torch.Tensor) else torch.from_numpy(e)).to(count_device)
             acc[0] += e_t.sum()
             acc[1] += (e_t > 0).sum()
@@ -124,19 +149,22 @@ def _run_point_all(generate, decode, K, ebn0_db, batch, max_blocks, world, rank,
 
 
 def run_point(generate, decode, K: int, ebn0_db: float, batch: int, max_blocks: int, stop_blkerrs: int | None = 1000,
-              A: int | None = None, group=None, count_device="cpu") -> PointResult:
+              A: int | None = None, group=None, count_device="cpu", gen_decode=None) -> PointResult:
     """Run one Eb/N0 point.  ``generate(frame0, B) -> (msg, sym)`` and
-    ``decode(sym) -> bits`` are this rank's frame source and decoder;
-    ``group`` is a torch.distributed process group (None = single process).
-    ``stop_blkerrs=None``: no early stop (every frame up to max_blocks)."""
+    ``decode(sym) -> bits`` are this rank's frame source and decoder, or
+    ``gen_decode(frame0, B) -> (msg, bits)`` does both in one call
+    (GpuFrames.decode_frames); ``group`` is a torch.distributed process group
+    (None = single process).  ``stop_blkerrs=None``: no early stop (every
+    frame up to max_blocks)."""
     import torch
     import torch.distributed as dist
 
     A = K if A is None else A
     world = dist.get_world_size(group) if group is not None else 1
     rank = dist.get_rank(group) if group is not None else 0
+    step_fn = _step_fn(generate, decode, gen_decode)
     if stop_blkerrs is None:
-        return _run_point_all(generate, decode, K, ebn0_db, batch, max_blocks, world, rank, group, count_device)
+        return _run_point_all(step_fn, K, ebn0_db, batch, max_blocks, world, rank, group, count_device)
     bit_errs = blk_errs = 0
     blocks = 0
     f0 = 0
@@ -145,8 +173,8 @@ def run_point(generate, decode, K: int, ebn0_db: float, batch: int, max_blocks: 
         lo = f0 + min(rank * batch, step)
         hi = f0 + min((rank + 1) * batch, step)
         if hi > lo:
-            msg, sym = generate(lo, hi - lo)
-            e = _frame_errors(decode(sym), msg)
+            msg, bits = step_fn(lo, hi - lo)
+            e = _frame_errors(bits, msg)
             e_t = e if isinstance(e, torch.Tensor) else torch.from_numpy(e)
             e_t = e_t.to(count_device)
             local = torch.stack([e_t.sum(), (e_t > 0).sum()]).to(torch.int64)
@@ -200,7 +228,7 @@ def simulate(decoder, msgbits_count: int, ebn0_list, *, seed: int = 2024, batch:
         # CRC-aided decoders output A bits: errors are counted over A, and the
         # driver's BER denominators are A (early stop) / K (MaxBlock), :185,196
         res = run_point(src, decoder.decode_batch, decoder.K, eb, batch, max_blocks, stop_blkerrs, A=decoder.out_bits,
-                        group=group, count_device=src.device)
+                        group=group, count_device=src.device, gen_decode=src.decode_frames)
         torch.cuda.synchronize()
         out.append(res)
     return out

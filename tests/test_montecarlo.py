@@ -233,3 +233,40 @@ def _pw_big(N, K):
     fm = np.ones(N, dtype=np.int64)
     fm[mb] = 0
     return mb, fm, 1 - fm
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,N,K,L,engine", [("SCL-LUT", 1024, 512, 8, "auto"), ("FastSCL-LUT", 1024, 512, 8, "auto"),
+                                               ("SC-LUT", 128, 32, 1, "auto"), ("CA-SCL-LUT", 256, 124, 8, "auto"),
+                                               ("SCL-LUT", 256, 128, 4, "generic")])
+def test_gpu_fused_generate_decode_equals_unfused(kind, N, K, L, engine, native_lib):
+    """qpd_mc_decode (generation writes the decoder's root pre-pass rows on a
+    fast-engine decoder, else its own symbol buffer) = qpd_mc_frames followed
+    by decode_batch, bit for bit, and so are the Monte-Carlo counters of a
+    fixed-seed point (the driver's stop rule and MaxBlock branch)."""
+    import torch
+
+    import quantized_decoder_polar_codes_amd as Q
+    from quantized_decoder_polar_codes_amd import codes as C
+    from quantized_decoder_polar_codes_amd import lutgen as LG
+
+    _, mb, fm, mm = C.construct_pw(N, K)
+    nt = C.identify_nodes(N, mb).astype(np.int32)
+    d = LG.design(N, 16, 3.0)
+    kw = {"A": K - 24} if kind.startswith("CA-") else {}
+    dec = Q.from_packed(kind, d.packed(), K, fm, L=L, node_type=nt, engine=engine, **kw)
+    sigma = MC.sigma_for(2.0, K / N)
+    _, _, edges, clut = LG.channel_quantizer(sigma, 128, 16)
+    src = MC.GpuFrames(dec, edges, clut, 16, sigma, seed=4321)
+    msg_a, sym = src(5000, 3001)
+    bits_a = dec.decode_batch(sym)
+    msg_b, bits_b = src.decode_frames(5000, 3001)
+    torch.cuda.synchronize()
+    assert torch.equal(msg_a, msg_b)
+    assert torch.equal(bits_a, bits_b)
+    for stop in (None, 50):
+        a = MC.run_point(src, dec.decode_batch, dec.K, 2.0, 1000, 7000, stop, A=dec.out_bits, count_device=src.device)
+        b = MC.run_point(src, dec.decode_batch, dec.K, 2.0, 1000, 7000, stop, A=dec.out_bits, count_device=src.device,
+                         gen_decode=src.decode_frames)
+        assert (a.bit_errors, a.block_errors, a.blocks, a.stopped_early) == \
+            (b.bit_errors, b.block_errors, b.blocks, b.stopped_early)
