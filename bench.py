@@ -332,15 +332,14 @@ def e2e_rate(args, ctx, wl):
     fused = getattr(src, "decode_frames", None)  # qpd_mc_decode: generation feeds the decode kernel
 
     def step():
-        if fused is not None:
-            msg, bits = fused(state["f0"], args.frames)
+        if fused is not None:  # counters accumulated on the device by the same call
+            fused(state["f0"], args.frames, counts=acc)
         else:  # a frame source without the fused call (the CPU tests' stand-in)
             msg, sym = src(state["f0"], args.frames)
-            bits = dec.decode_batch(sym)
+            e = (dec.decode_batch(sym) != msg).sum(1)
+            acc[0] += e.sum()
+            acc[1] += (e > 0).sum()
         state["f0"] += args.frames
-        e = (bits != msg).sum(1)
-        acc[0] += e.sum()
-        acc[1] += (e > 0).sum()
 
     if prof:
         dec.profile(True)

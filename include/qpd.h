@@ -242,10 +242,12 @@ int qpd_mc_frames(qpd_decoder *dec, const qpd_mc_channel *ch, uint64_t seed, int
  * qpd_mc_frames generates with the same arguments (d_msg as there), without
  * materializing the int32 symbols -- on a fast-engine decoder in pre-mode the
  * generator writes the root pre-pass rows the decode kernel reads (LUT kinds;
- * q <= v).  The driver's loop body (mainQuantizedDecoder_LLRDomain.py:151-178)
- * in one call; the error count stays with the caller. */
+ * q <= v).  d_counts (device int64[2], or NULL): bit errors and block errors of
+ * the B frames (d_out against d_msg) are ADDED to it, the driver's counters
+ * (:181-183).  The driver's loop body (mainQuantizedDecoder_LLRDomain.py:151-183)
+ * in one call. */
 int qpd_mc_decode(qpd_decoder *dec, const qpd_mc_channel *ch, uint64_t seed, int64_t frame0, int64_t B,
-                  uint8_t *d_msg, uint8_t *d_out, void *stream);
+                  uint8_t *d_msg, uint8_t *d_out, int64_t *d_counts, void *stream);
 
 /*
  * Offline table design (host code, no device needed) -- the reference's

@@ -168,7 +168,7 @@ def load():
     L.qpd_get_info.restype = ctypes.c_int
     L.qpd_mc_frames.argtypes = [_P, ctypes.POINTER(QpdMcChannel), ctypes.c_uint64, _i64, _i64, _P, _P, _P]
     L.qpd_mc_frames.restype = ctypes.c_int
-    L.qpd_mc_decode.argtypes = [_P, ctypes.POINTER(QpdMcChannel), ctypes.c_uint64, _i64, _i64, _P, _P, _P]
+    L.qpd_mc_decode.argtypes = [_P, ctypes.POINTER(QpdMcChannel), ctypes.c_uint64, _i64, _i64, _P, _P, _P, _P]
     L.qpd_mc_decode.restype = ctypes.c_int
     L.qpd_optls_quantizer.argtypes = [_P, _P, _i32, _i32, _i32, _P, _P, _P, _P]
     L.qpd_optls_quantizer.restype = ctypes.c_int

@@ -1249,11 +1249,16 @@ int mc_launch(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64_t f
     C.g_tab = d->fplan.g_tab;
     for (int i = 0; i < ch->n_edges; ++i) C.edges[i] = ch->edges[i];
     for (int i = 0; i + 1 < ch->n_edges; ++i) C.lut[i] = ch->lut[i];
-    int dev = 0, ncu = 256;
+    int dev = 0, ncu = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    const int grid = (int)std::min<int64_t>(B, (int64_t)ncu * 32);
     const size_t lds = qpd::mc_lds_bytes(d->N, d->K, pre);
+    // one resident round of workgroups (grid-stride over frames): a grid
+    // larger than what fits at once runs its last workgroups as a tail
+    const void *kfn = pre ? reinterpret_cast<const void *>(&qpd::mc_frames_kernel<true>)
+                          : reinterpret_cast<const void *>(&qpd::mc_frames_kernel<false>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 64, lds) != hipSuccess || per_cu <= 0) per_cu = 8;
+    const int grid = (int)std::min<int64_t>(B, (int64_t)ncu * per_cu);
     return timed_launch(d, QPD_KC_MC, st, [&]() -> int {
         if (pre)
             hipLaunchKernelGGL(qpd::mc_frames_kernel<true>, dim3(grid), dim3(64), lds, st, C, frame0, B, d_msg, rows);
@@ -1444,7 +1449,7 @@ int qpd_mc_frames(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64
 }
 
 int qpd_mc_decode(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64_t frame0, int64_t B, uint8_t *d_msg,
-                  uint8_t *d_out, void *stream) {
+                  uint8_t *d_out, int64_t *d_counts, void *stream) {
     if (!d || !ch) return fail(QPD_E_INVALID, "null argument");
     if (d->dom != qpd::DOM_LUT) return fail(QPD_E_INVALID, "qpd_mc_decode needs a LUT decoder (int32 channel symbols)");
     if (B < 0 || frame0 < 0) return fail(QPD_E_INVALID, "negative frame range");
@@ -1482,6 +1487,15 @@ int qpd_mc_decode(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64
             r = fused ? decode_pre_rows(d, (const uint32_t *)buf.p, Bc, out, st)
                       : decode_impl(d, (const int32_t *)buf.p, Bc, out, st);
             if (r) return r;
+        }
+        if (d_counts) {  // the driver's error counters over the whole range
+            int dev = 0, ncu = 256;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((B + 3) / 4, (int64_t)ncu * 8));
+            hipLaunchKernelGGL(qpd::mc_count_kernel, dim3(grid), dim3(256), 0, st, d_out, d_msg, B, d->out_bits,
+                               (unsigned long long *)d_counts);
+            QPD_HIP(hipGetLastError());
         }
         return QPD_OK;
     });

@@ -217,6 +217,7 @@ __global__ __launch_bounds__(64) void mc_frames_kernel(McChannel C, int64_t fram
             const double nz[2] = {rad * cs, rad * sn};
             const uint32_t xbits = xw[(2 * p) >> 5] >> ((2 * p) & 31);
             int s_out[2];
+#pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const double bpsk = (xbits >> h) & 1u ? -1.0 : 1.0;
                 const double y = bpsk + C.sigma * nz[h];
@@ -264,6 +265,37 @@ __global__ __launch_bounds__(64) void mc_frames_kernel(McChannel C, int64_t fram
             }
             __syncthreads();
         }
+    }
+}
+
+// Bit and block errors of decoded frames against their messages, added to
+// counts[0] / counts[1] (the driver's counters, mainQuantizedDecoder_LLRDomain.py:181-183):
+// one wave per frame (grid-stride), 8 bytes per lane per step -- the bytes are
+// 0 / 1, so popcount(a ^ b) counts the differing ones -- two atomics per wave.
+__global__ __launch_bounds__(256) void mc_count_kernel(const uint8_t *__restrict__ bits,
+                                                       const uint8_t *__restrict__ msg, int64_t B, int K,
+                                                       unsigned long long *__restrict__ counts) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    unsigned long long be = 0, fe = 0;
+    const bool vec = (K & 7) == 0 && ((uintptr_t)bits & 7) == 0 && ((uintptr_t)msg & 7) == 0;
+    for (int64_t f = wave; f < B; f += waves) {
+        const uint8_t *a = bits + f * K, *b = msg + f * K;
+        unsigned e = 0;
+        if (vec) {
+            for (int i = 8 * lane; i < K; i += 512)
+                e += __popcll(*(const unsigned long long *)(a + i) ^ *(const unsigned long long *)(b + i));
+        } else {
+            for (int i = lane; i < K; i += 64) e += (a[i] ^ b[i]) & 1u;
+        }
+        for (int m = 32; m >= 1; m >>= 1) e += (unsigned)__shfl_xor((int)e, m, 64);
+        be += e;
+        fe += e != 0;
+    }
+    if (lane == 0 && be) {
+        atomicAdd(counts, be);
+        atomicAdd(counts + 1, fe);
     }
 }
 

@@ -74,16 +74,18 @@ class GpuFrames:
         self.seed = int(seed)
         self.device = torch.device("cuda", decoder.device if decoder.device >= 0 else torch.cuda.current_device())
 
-    def decode_frames(self, frame0: int, B: int):
+    def decode_frames(self, frame0: int, B: int, counts=None):
         """(msg, decoded bits) of frames [frame0, frame0+B): the same bits as
         decode_batch(self(frame0, B)[1]), by qpd_mc_decode (generation feeds the
-        decode kernel's pre-pass rows directly, no int32 symbols)."""
+        decode kernel's pre-pass rows directly, no int32 symbols).  ``counts``:
+        a device int64[2] tensor the frames' bit and block errors are added to."""
         torch = self.torch
         msg = torch.empty((B, self.dec.out_bits), dtype=torch.uint8, device=self.device)
         bits = torch.empty((B, self.dec.out_bits), dtype=torch.uint8, device=self.device)
         stream = torch.cuda.current_stream(self.device).cuda_stream
+        cp = ctypes.c_void_p(counts.data_ptr()) if counts is not None else None
         _lib.check(_lib.load().qpd_mc_decode(self.dec._h, ctypes.byref(self.ch), ctypes.c_uint64(self.seed), frame0, B,
-                                             ctypes.c_void_p(msg.data_ptr()), ctypes.c_void_p(bits.data_ptr()),
+                                             ctypes.c_void_p(msg.data_ptr()), ctypes.c_void_p(bits.data_ptr()), cp,
                                              ctypes.c_void_p(stream)))
         return msg, bits
 
@@ -122,9 +124,11 @@ def _step_fn(generate, decode, gen_decode):
     return step
 
 
-def _run_point_all(step_fn, K, ebn0_db, batch, max_blocks, world, rank, group, count_device):
+def _run_point_all(step_fn, K, ebn0_db, batch, max_blocks, world, rank, group, count_device, counted=None):
     """run_point without early stop (the driver's MaxBlock branch, :194-196):
-    counters accumulate on the device, one all-reduce at the end."""
+    counters accumulate on the device, one all-reduce at the end.
+    ``counted(frame0, B, counts)``: a fused call that also adds the frames'
+    errors to the device counters (GpuFrames.decode_frames)."""
     import torch
     import torch.distributed as dist
 
@@ -135,11 +139,14 @@ def _run_point_all(step_fn, K, ebn0_db, batch, max_blocks, world, rank, group, c
         lo = f0 + min(rank * batch, step)
         hi = f0 + min((rank + 1) * batch, step)
         if hi > lo:
-            msg, bits = step_fn(lo, hi - lo)
-            e = _frame_errors(bits, msg)
-            e_t = (e if isinstance(e, torch.Tensor) else torch.from_numpy(e)).to(count_device)
-            acc[0] += e_t.sum()
-            acc[1] += (e_t > 0).sum()
+            if counted is not None and acc.is_cuda:
+                counted(lo, hi - lo, acc)
+            else:
+                msg, bits = step_fn(lo, hi - lo)
+                e = _frame_errors(bits, msg)
+                e_t = (e if isinstance(e, torch.Tensor) else torch.from_numpy(e)).to(count_device)
+                acc[0] += e_t.sum()
+                acc[1] += (e_t > 0).sum()
         f0 += step
     if group is not None:
         dist.all_reduce(acc, group=group)
@@ -164,7 +171,8 @@ def run_point(generate, decode, K: int, ebn0_db: float, batch: int, max_blocks: 
     rank = dist.get_rank(group) if group is not None else 0
     step_fn = _step_fn(generate, decode, gen_decode)
     if stop_blkerrs is None:
-        return _run_point_all(step_fn, K, ebn0_db, batch, max_blocks, world, rank, group, count_device)
+        counted = (lambda lo, n, acc: gen_decode(lo, n, counts=acc)) if gen_decode is not None else None
+        return _run_point_all(step_fn, K, ebn0_db, batch, max_blocks, world, rank, group, count_device, counted)
     bit_errs = blk_errs = 0
     blocks = 0
     f0 = 0
