@@ -1241,7 +1241,7 @@ int mc_launch(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64_t f
     C.seed_lo = (uint32_t)seed;
     C.seed_hi = (uint32_t)(seed >> 32);
     C.sigma = ch->sigma;
-    C.s2 = ch->sigma * ch->sigma;
+    C.inv_s2 = 1.0 / (ch->sigma * ch->sigma);  // the driver's sigma ** 2, inverted once
     C.info_mask = (const uint32_t *)d->info_mask.p;
     C.info_pref = (const int32_t *)d->mc_pref.p;
     C.crc_tab = (const uint32_t *)d->mc_crc.p;

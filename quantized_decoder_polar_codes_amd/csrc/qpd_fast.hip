@@ -279,11 +279,9 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
     if (ctemp >= 64) {
         const int nwo = ctemp >> 3;  // multiple of 8
         if constexpr (NS >= 2) {
-            // chunks of 4 words of both sets, software-pipelined: the next
-            // chunk's loads (slab rows of the shallow depths: HBM latency) are
-            // in flight while the current chunk's lookups run
-            uint32_t A[NS][4], B[NS][4], ub[NS];
-            auto load = [&](int w0) {
+            // chunks of 4 words of both sets: the sets' loads are in flight together
+            for (int w0 = 0; w0 < nwo; w0 += 4) {
+                uint32_t A[NS][4], B[NS][4], ub[NS];
 #pragma unroll
                 for (int s = 0; s < NS; ++s) {
 #pragma unroll
@@ -293,25 +291,11 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
                     }
                     ub[s] = ISG ? M[s].ld(ul, op.u_row + (w0 >> 2), usrc[s]) : 0u;
                 }
-            };
-            load(0);
-            for (int w0 = 0; w0 < nwo; w0 += 4) {
-                uint32_t cA[NS][4], cB[NS][4], cub[NS];
-#pragma unroll
-                for (int s = 0; s < NS; ++s) {
-                    cub[s] = ub[s];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        cA[s][k] = A[s][k];
-                        cB[s][k] = B[s][k];
-                    }
-                }
-                if (w0 + 4 < nwo) load(w0 + 4);
 #pragma unroll
                 for (int s = 0; s < NS; ++s)
 #pragma unroll
                     for (int k = 0; k < 4; ++k)
-                        M[s].st(dl, op.dst_row + w0 + k, lane, lut_vec<8>(T, cA[s][k], cB[s][k], cub[s] >> (k << 3)));
+                        M[s].st(dl, op.dst_row + w0 + k, lane, lut_vec<8>(T, A[s][k], B[s][k], ub[s] >> (k << 3)));
             }
         } else {
             for (int w0 = 0; w0 < nwo; w0 += 8) {
@@ -382,45 +366,6 @@ __device__ __forceinline__ void gsel_op(const Mem (&M)[NS], const MOp &op, const
                                         const int (&usrc)[NS], int lane) {
     const int nwo = op.cnt >> 3;  // 1, 2, 4 or a multiple of 8
     const bool dl = op.flags & MF_DST_LDS, ul = op.flags & MF_U_LDS;
-    if (nwo >= 4 && (nwo & 3) == 0) {
-        // chunks of 4 words of every set, software-pipelined as in fg_op:
-        // the next chunk's pre-pass and U loads fly during the selects
-        uint32_t g0[NS][4], g1[NS][4], u[NS];
-        auto load = [&](int w0) {
-#pragma unroll
-            for (int s = 0; s < NS; ++s) {
-                const uint32_t *g = (const uint32_t *)y[s] + op.src_row;  // g(y, 0) words; g(y, 1) at + nwo
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    g0[s][k] = g[w0 + k];
-                    g1[s][k] = g[nwo + w0 + k];
-                }
-                u[s] = M[s].ld(ul, op.u_row + (w0 >> 2), usrc[s]);
-            }
-        };
-        load(0);
-        for (int w0 = 0; w0 < nwo; w0 += 4) {
-            uint32_t c0[NS][4], c1[NS][4], cu[NS];
-#pragma unroll
-            for (int s = 0; s < NS; ++s) {
-                cu[s] = u[s];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    c0[s][k] = g0[s][k];
-                    c1[s][k] = g1[s][k];
-                }
-            }
-            if (w0 + 4 < nwo) load(w0 + 4);
-#pragma unroll
-            for (int s = 0; s < NS; ++s)
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t m = nib_mask(cu[s] >> (k << 3));
-                    M[s].st(dl, op.dst_row + w0 + k, lane, c0[s][k] ^ ((c0[s][k] ^ c1[s][k]) & m));
-                }
-        }
-        return;
-    }
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const uint32_t *g = (const uint32_t *)y[s] + op.src_row;  // g(y, 0) words; g(y, 1) at + nwo
@@ -1250,10 +1195,9 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
                         int usrc[NS];
 #pragma unroll
                         for (int s = 0; s < NS; ++s) usrc[s] = gbase + pfield(stv[s].pu, op.sh_u);
-                        // 4 words of every set per round, software-pipelined:
-                        // the next round's loads fly during this round's stores
-                        uint32_t u[NS][4], r[NS][4];
-                        auto load = [&](int w0) {
+                        // 4 words of every set per round: all their loads in flight together
+                        for (int w0 = 0; w0 < cw; w0 += 4) {
+                            uint32_t u[NS][4], r[NS][4];
 #pragma unroll
                             for (int s = 0; s < NS; ++s)
 #pragma unroll
@@ -1264,25 +1208,13 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
                                         r[s][k] = Mv[s].ld(rl, op.r_row + w0 + k, lane);
                                     }
                                 }
-                        };
-                        load(0);
-                        for (int w0 = 0; w0 < cw; w0 += 4) {
-                            uint32_t cu[NS][4], cr[NS][4];
-#pragma unroll
-                            for (int s = 0; s < NS; ++s)
-#pragma unroll
-                                for (int k = 0; k < 4; ++k) {
-                                    cu[s][k] = u[s][k];
-                                    cr[s][k] = r[s][k];
-                                }
-                            if (w0 + 4 < cw) load(w0 + 4);
 #pragma unroll
                             for (int s = 0; s < NS; ++s)
 #pragma unroll
                                 for (int k = 0; k < 4; ++k)
                                     if (k == 0 || w0 + k < cw) {
-                                        Mv[s].st(dl, op.dst_row + w0 + k, lane, cu[s][k] ^ cr[s][k]);
-                                        Mv[s].st(dl, op.dst_row + cw + w0 + k, lane, cr[s][k]);
+                                        Mv[s].st(dl, op.dst_row + w0 + k, lane, u[s][k] ^ r[s][k]);
+                                        Mv[s].st(dl, op.dst_row + cw + w0 + k, lane, r[s][k]);
                                     }
                         }
                     }

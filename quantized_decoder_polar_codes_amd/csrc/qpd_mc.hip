@@ -4,8 +4,9 @@
 // (mainQuantizedDecoder_LLRDomain.py:151-176): message bits, optional CRC
 // (CRCEnc, :153-156), polar encoding (the un-vendored PolarEnc, restated:
 // u[info] = msg, x = u F^{(x)n} in natural order), BPSK, AWGN in float64
-// (`y = bpsk + normal(0, sigma)`, `llr = y * 2 / sigma**2`, :161-165, with the
-// same roundings: no fused multiply-add) and the driver's channel quantizer
+// (`y = bpsk + normal(0, sigma)`, `llr = y * 2 / sigma**2`, :161-165, no fused
+// multiply-add; the division by sigma**2 is a multiplication by its reciprocal,
+// within an ulp of the driver's quotient) and the driver's channel quantizer
 // (saturate at the outer edges, else channel_lut[bisect_left(edges[:-1], llr) - 1],
 // :167-176).
 //
@@ -16,9 +17,10 @@
 // frames.  Gaussians: Box-Muller in float64 on 53-bit
 // uniforms (two Philox words each), u1 in (0, 1], u2 in [0, 1).
 //
-// bisect_left is exact for any ascending edges: the walk from a guess ends at
-// the first edge >= llr whatever the guess (uniform edges, the driver's
-// linspace, need 0-1 steps).
+// bisect_left is exact for any ascending edges: a guess from the mean bin
+// width, checked against its two neighbouring edges (one LDS read); only a
+// wrong guess walks, and the walk ends at the first edge >= llr whatever the
+// guess (uniform edges, the driver's linspace, are almost never wrong).
 //
 // PRE mode (qpd_mc_decode): the frame's symbols are staged in LDS and the
 // kernel writes the decoder's root pre-pass row instead (root_pre_kernel,
@@ -47,6 +49,7 @@ struct Philox4 {
 
 __host__ __device__ inline Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
                                                   uint32_t k1) {
+#pragma unroll
     for (int r = 0; r < 10; ++r) {
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
@@ -70,7 +73,7 @@ __host__ __device__ inline Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint3
 struct McChannel {
     int32_t N, K, q, n_edges;
     int32_t A, crc_n;     // crc_n > 0: A message bits + first K-A bits of their CRC
-    double sigma, s2;     // AWGN std and sigma*sigma (the driver's sigma ** 2)
+    double sigma, inv_s2; // AWGN std and 1 / (sigma*sigma): llr = (2y) * inv_s2
     uint32_t seed_lo, seed_hi;
     const uint32_t *info_mask;  // [N/32] bit i of word w: position 32w+i is an information bit
     const int32_t *info_pref;   // [N/32] information bits before word w
@@ -109,12 +112,37 @@ __device__ inline void mc_sincos(double x, double *sn, double *cs) {
                                       -1.38888888888741095749e-03), 4.16666666666666019037e-02);
     const double hz = 0.5 * z, w = 1.0 - hz;
     const double cr = w + (((1.0 - w) - hz) + z * pc);
-    switch ((int)q & 3) {
-        case 0: *sn = sr; *cs = cr; break;
-        case 1: *sn = cr; *cs = -sr; break;
-        case 2: *sn = -sr; *cs = -cr; break;
-        default: *sn = -cr; *cs = sr; break;
+    // quadrant q & 3: (sr, cr), (cr, -sr), (-sr, -cr), (-cr, sr) -- as selects
+    const int qi = (int)q;
+    const double s0 = (qi & 1) ? cr : sr, c0 = (qi & 1) ? sr : cr;
+    *sn = (qi & 2) ? -s0 : s0;
+    *cs = ((qi + 1) & 2) ? -c0 : c0;
+}
+
+// log(u) for u in (0, 1]: fdlibm's __ieee754_log (u = m 2^k with m in
+// [sqrt(2)/2, sqrt(2)), f = m - 1, s = f / (2 + f), the Remez polynomial in
+// s^2; < 1 ulp) with its one division as a Newton-refined reciprocal plus a
+// residual correction -- s enters only through s (hfsq + R), an O(f^3) term.
+// A third of the instructions of the double-double device log.
+__device__ inline double mc_log(double u) {
+    int k;
+    double m = frexp(u, &k);  // [0.5, 1)
+    if (m < 0.70710678118654752440) {
+        m += m;
+        --k;
     }
+    const double f = m - 1.0, dd = 2.0 + f;
+    double r = __builtin_amdgcn_rcp(dd);
+    r = fma(fma(-dd, r, 1.0), r, r);
+    r = fma(fma(-dd, r, 1.0), r, r);
+    double s = f * r;
+    s = fma(fma(-dd, s, f), r, s);
+    const double z = s * s, w = z * z;
+    const double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 + w * 1.531383769920937332e-01));
+    const double t2 = z * (6.666666666666735130e-01 +
+                           w * (2.857142874366239149e-01 + w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
+    const double R = t2 + t1, hfsq = 0.5 * f * f, dk = (double)k;
+    return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
 }
 
 template <bool PRE>
@@ -132,12 +160,14 @@ __global__ __launch_bounds__(64) void mc_frames_kernel(McChannel C, int64_t fram
     const int N = C.N, K = C.K, A = C.A, M = C.n_edges - 1;
     const int nw = (N + 31) >> 5;        // u / x words
     const int kw = (K + 31) >> 5;        // information-bit words (message + CRC)
-    double *edges = reinterpret_cast<double *>(lds_mc);
-    int32_t *lut = reinterpret_cast<int32_t *>(edges + kMcMaxEdges);
+    // E[0] = -inf, E[1 + i] = edges[i]: E[lo] = edges[lo - 1] and E[lo + 1] = edges[lo] need no guards
+    double *E = reinterpret_cast<double *>(lds_mc);
+    int32_t *lut = reinterpret_cast<int32_t *>(E + kMcMaxEdges + 1);
     uint32_t *xw = reinterpret_cast<uint32_t *>(lut + kMcMaxEdges);
     uint32_t *bw = xw + nw;               // message + CRC bits (kw + 2 words)
     uint8_t *sy = reinterpret_cast<uint8_t *>(bw + kw + 2);  // PRE: the frame's N channel symbols
-    for (int i = t; i < C.n_edges; i += 64) edges[i] = C.edges[i];
+    for (int i = t; i < C.n_edges; i += 64) E[1 + i] = C.edges[i];
+    if (t == 0) E[0] = -__builtin_inf();
     for (int i = t; i < M; i += 64) lut[i] = C.lut[i];
     const double lo_edge = C.edges[0], hi_edge = C.edges[M];
     const double inv_w = hi_edge > lo_edge ? M / (hi_edge - lo_edge) : 0.0;
@@ -150,18 +180,22 @@ __global__ __launch_bounds__(64) void mc_frames_kernel(McChannel C, int64_t fram
             uint32_t m = 0;
             if (32 * d < A) {
                 const Philox4 r = philox4x32_10(glo, ghi, (uint32_t)(d >> 2), kTagMsg, C.seed_lo, C.seed_hi);
-                m = r.v[d & 3];
+                // r.v[d & 3] as selects (a dynamic index would go through scratch)
+                const uint32_t lo2 = (d & 1) ? r.v[1] : r.v[0], hi2 = (d & 1) ? r.v[3] : r.v[2];
+                m = (d & 2) ? hi2 : lo2;
                 if (A - 32 * d < 32) m &= (1u << (A - 32 * d)) - 1u;
                 // msg bytes 32d .. 32d+31 (A % 8 == 0: 8 B stores)
                 uint8_t *mo = msg_out + f * A + 32 * d;
                 const int nb = min(32, A - 32 * d);
                 if ((A & 7) == 0 && nb == 32) {
                     uint32_t w4[8];
+#pragma unroll
                     for (int k = 0; k < 8; ++k) {
                         const uint32_t nib = (m >> (4 * k)) & 0xFu;
                         w4[k] = (nib & 1u) | ((nib & 2u) << 7) | ((nib & 4u) << 14) | ((nib & 8u) << 21);
                     }
                     uint2 *o2 = reinterpret_cast<uint2 *>(mo);
+#pragma unroll
                     for (int k = 0; k < 4; ++k) o2[k] = make_uint2(w4[2 * k], w4[2 * k + 1]);
                 } else {
                     for (int b = 0; b < nb; ++b) mo[b] = (uint8_t)((m >> b) & 1u);
@@ -211,7 +245,7 @@ __global__ __launch_bounds__(64) void mc_frames_kernel(McChannel C, int64_t fram
             const Philox4 r = philox4x32_10(glo, ghi, (uint32_t)p, kTagNoise, C.seed_lo, C.seed_hi);
             const double u1 = (double)(mc_u53(r.v[0], r.v[1]) + 1u) * 0x1p-53;  // (0, 1]
             const double u2 = (double)mc_u53(r.v[2], r.v[3]) * 0x1p-53;         // [0, 1)
-            const double rad = sqrt(-2.0 * log(u1));
+            const double rad = sqrt(-2.0 * mc_log(u1));
             double sn, cs;
             mc_sincos(6.283185307179586 * u2, &sn, &cs);
             const double nz[2] = {rad * cs, rad * sn};
@@ -221,18 +255,18 @@ __global__ __launch_bounds__(64) void mc_frames_kernel(McChannel C, int64_t fram
             for (int h = 0; h < 2; ++h) {
                 const double bpsk = (xbits >> h) & 1u ? -1.0 : 1.0;
                 const double y = bpsk + C.sigma * nz[h];
-                const double llr = y * 2.0 / C.s2;
-                if (llr <= lo_edge) {
-                    s_out[h] = 0;
-                } else if (llr >= hi_edge) {
-                    s_out[h] = C.q - 1;
-                } else {  // bisect_left over edges[0..M-1]: a guess from the mean bin width, then walk
-                    int lo = (int)((llr - lo_edge) * inv_w);
-                    lo = lo < 0 ? 0 : (lo > M ? M : lo);
-                    while (lo > 0 && edges[lo - 1] >= llr) --lo;
-                    while (lo < M && edges[lo] < llr) ++lo;
-                    s_out[h] = lut[lo - 1];
+                const double llr = y * 2.0 * C.inv_s2;
+                // bisect_left over edges[0..M-1] for lo_edge < llr < hi_edge: lo in [1, M]
+                // with edges[lo - 1] < llr <= edges[lo]; guessed, checked, walked if wrong
+                const bool inner = llr > lo_edge && llr < hi_edge;
+                const double gi = fmin(fmax((llr - lo_edge) * inv_w + 1.0, 1.0), (double)M);
+                int lo = (int)gi;
+                if (inner && !(E[lo] < llr && llr <= E[lo + 1])) {
+                    while (E[lo] >= llr) --lo;     // stops at lo >= 1: E[1] = lo_edge < llr
+                    while (E[lo + 1] < llr) ++lo;  // stops at lo <= M: E[M + 1] = hi_edge > llr
                 }
+                const int sl = lut[lo - 1];
+                s_out[h] = inner ? sl : (llr <= lo_edge ? 0 : C.q - 1);
             }
             if (PRE)
                 *reinterpret_cast<uint16_t *>(sy + 2 * p) = (uint16_t)(s_out[0] | (s_out[1] << 8));
@@ -301,7 +335,7 @@ __global__ __launch_bounds__(256) void mc_count_kernel(const uint8_t *__restrict
 
 // Dynamic LDS of mc_frames_kernel.
 inline size_t mc_lds_bytes(int N, int K, bool pre) {
-    return kMcMaxEdges * (sizeof(double) + sizeof(int32_t)) + 4 * (((N + 31) >> 5) + ((K + 31) >> 5) + 2) +
+    return (kMcMaxEdges + 1) * sizeof(double) + kMcMaxEdges * sizeof(int32_t) + 4 * (((N + 31) >> 5) + ((K + 31) >> 5) + 2) +
            (pre ? (size_t)N : 0);
 }
 

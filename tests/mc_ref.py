@@ -53,6 +53,7 @@ def frames(N, K, msgbits, seed, frame0, B, sigma, edges, lut, q, A=None, crc=Non
     x = C.polar_encode(u, msgbits, N)
     llr = np.zeros((B, N), dtype=np.float64)
     s2 = np.float64(sigma) * np.float64(sigma)  # the driver's sigma ** 2
+    inv_s2 = 1.0 / s2
     for p in range(N // 2):
         r = philox(glo, ghi, np.full(B, p, np.uint64), np.full(B, TAG_NOISE, np.uint64), slo, shi)
         u1 = (u53(r[0], r[1]) + np.uint64(1)).astype(np.float64) * 2.0 ** -53  # (0, 1]
@@ -63,6 +64,6 @@ def frames(N, K, msgbits, seed, frame0, B, sigma, edges, lut, q, A=None, crc=Non
         for h in range(2):
             e = 2 * p + h
             y = (1.0 - 2.0 * x[:, e].astype(np.float64)) + np.float64(sigma) * nz[h]  # y = bpsk + normal(0, sigma)
-            llr[:, e] = y * 2.0 / s2  # mainQuantizedDecoder_LLRDomain.py:165
+            llr[:, e] = y * 2.0 * inv_s2  # mainQuantizedDecoder_LLRDomain.py:165 (y * 2 / sigma**2), as the generator: x reciprocal
     sym = C.quantize_channel(llr, edges, lut, q)
     return msg, sym, llr
