@@ -14,7 +14,7 @@
 // Philox4x32-10 with counter = (frame_lo, frame_hi, word, stream tag), so a
 // frame's content does not depend on batch size, grid, or how frames are
 // sharded across GPUs -- the 1/2/4/8-GPU runs of one frame range see the same
-// frames.  Gaussians: Box-Muller in float64 on 53-bit
+// frames.  Gaussians: Box-Muller in float64 on 52-bit
 // uniforms (two Philox words each), u1 in (0, 1], u2 in [0, 1).
 //
 // bisect_left is exact for any ascending edges: a guess from the mean bin
@@ -47,7 +47,7 @@ struct Philox4 {
     uint32_t v[4];
 };
 
-__host__ __device__ inline Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+__device__ inline Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
                                                   uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
@@ -61,6 +61,9 @@ __host__ __device__ inline Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint3
         c3 = (uint32_t)p0;
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
+        // the round keys stay two SGPRs advanced per round (SALU) instead of
+        // 20 hoisted loop invariants, which would spill the kernel's SGPRs
+        asm volatile("" : "+s"(k0), "+s"(k1));
     }
     Philox4 o;
     o.v[0] = c0;
@@ -87,9 +90,10 @@ struct McChannel {
     const uint32_t *f_tab, *g_tab;  // node 0's nibble tables (FastPlan f_tab / g_tab)
 };
 
-// 53-bit uniform from two Philox words: k = (a >> 5) * 2^26 + (b >> 6), k * 2^-53.
-__device__ __host__ inline uint64_t mc_u53(uint32_t a, uint32_t b) {
-    return ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
+// The double 1.m in [1, 2) whose 52 mantissa bits are (a >> 12) : b -- two
+// Philox words; 2 - x is then uniform on (0, 1], x - 1 on [0, 1) (52-bit grid).
+__device__ __host__ inline double mc_one_m(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(double, ((uint64_t)(0x3FF00000u | (a >> 12)) << 32) | b);
 }
 
 // sin and cos of x in [0, 2 pi] for the Box-Muller angle: reduction by
@@ -138,15 +142,19 @@ __device__ inline double mc_log(double u) {
     double s = f * r;
     s = fma(fma(-dd, s, f), r, s);
     const double z = s * s, w = z * z;
-    const double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 + w * 1.531383769920937332e-01));
-    const double t2 = z * (6.666666666666735130e-01 +
-                           w * (2.857142874366239149e-01 + w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
+    // fdlibm's Horner steps as fused multiply-adds
+    const double t1 = w * fma(w, fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01), 3.999999999940941908e-01);
+    const double t2 = z * fma(w, fma(w, fma(w, 1.479819860511658591e-01, 1.818357216161805012e-01), 2.857142874366239149e-01),
+                              6.666666666666735130e-01);
     const double R = t2 + t1, hfsq = 0.5 * f * f, dk = (double)k;
     return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
 }
 
+#ifndef QPD_MC_WPE
+#define QPD_MC_WPE 6  // 6 waves per SIMD: -2.5 % generator time vs 5 (profiles/r03j_ab_generator.txt)
+#endif
 template <bool PRE>
-__global__ __launch_bounds__(64) void mc_frames_kernel(McChannel C, int64_t frame0, int64_t B,
+__global__ __launch_bounds__(64, QPD_MC_WPE) void mc_frames_kernel(McChannel C, int64_t frame0, int64_t B,
                                                        uint8_t *__restrict__ msg_out, int32_t *__restrict__ sym_out) {
 #pragma clang fp contract(off)
     extern __shared__ uint32_t lds_mc[];
@@ -215,24 +223,32 @@ __global__ __launch_bounds__(64) void mc_frames_kernel(McChannel C, int64_t fram
                 }
         }
         __syncthreads();
-        // u word w = the info bits [pref_w, pref_w + popc(mask_w)) deposited at the mask's set bits;
+        // u word w = the info bits [pref_w, pref_w + popc(mask_w)) deposited at the mask's set bits,
+        // one 16-bit half per lane (the deposit loop runs popc(half) <= 16 times);
         // then the 5 in-word stages of x = u F^{(x)n} (bit i ^= bit i + m for i with bit m clear)
-        for (int w = t; w < nw; w += 64) {
-            uint32_t mask = C.info_mask[w];
-            const int s = C.info_pref[w];
-            const uint32_t lo = bw[s >> 5], hi = bw[(s >> 5) + 1];
-            uint32_t src = (s & 31) ? ((lo >> (s & 31)) | (hi << (32 - (s & 31)))) : lo;
+        for (int h0 = 0; h0 < 2 * nw; h0 += 64) {  // whole-wave rounds: the halves meet by a shuffle
+            const int h = h0 + t, w = h >> 1;
             uint32_t u = 0;
-            for (; mask; mask &= mask - 1u) {
-                u |= (src & 1u) << __builtin_ctz(mask);
-                src >>= 1;
+            if (h < 2 * nw) {
+                const uint32_t wm = C.info_mask[w];
+                uint32_t mask = (h & 1) ? wm >> 16 : wm & 0xFFFFu;
+                const int s = C.info_pref[w] + ((h & 1) ? __builtin_popcount(wm & 0xFFFFu) : 0);
+                const uint32_t lo = bw[s >> 5], hi = bw[(s >> 5) + 1];
+                uint32_t src = (s & 31) ? ((lo >> (s & 31)) | (hi << (32 - (s & 31)))) : lo;
+                for (; mask; mask &= mask - 1u) {
+                    u |= (src & 1u) << __builtin_ctz(mask);
+                    src >>= 1;
+                }
             }
-            u ^= (u >> 1) & 0x55555555u;
-            u ^= (u >> 2) & 0x33333333u;
-            u ^= (u >> 4) & 0x0F0F0F0Fu;
-            u ^= (u >> 8) & 0x00FF00FFu;
-            u ^= (u >> 16) & 0x0000FFFFu;
-            xw[w] = u;
+            u |= (uint32_t)__shfl_xor((int)u, 1, 64) << 16;  // even lane: low | high << 16
+            if (h < 2 * nw && !(h & 1)) {
+                u ^= (u >> 1) & 0x55555555u;
+                u ^= (u >> 2) & 0x33333333u;
+                u ^= (u >> 4) & 0x0F0F0F0Fu;
+                u ^= (u >> 8) & 0x00FF00FFu;
+                u ^= (u >> 16) & 0x0000FFFFu;
+                xw[w] = u;
+            }
         }
         __syncthreads();
         for (int sw = 1; sw < nw; sw <<= 1) {  // word stages (m = 32 sw)
@@ -240,15 +256,20 @@ __global__ __launch_bounds__(64) void mc_frames_kernel(McChannel C, int64_t fram
                 if (!(w & sw)) xw[w] ^= xw[w + sw];
             __syncthreads();
         }
-        // AWGN + LLR + channel quantizer, positions 2p and 2p+1
-        for (int p = t; 2 * p < N; p += 64) {
+        // AWGN + LLR + channel quantizer, positions 2p and 2p+1, two pairs per
+        // lane and round (p and p + 64): their Philox / log / sincos chains are
+        // independent straight-line code the scheduler interleaves
+        auto noise = [&](int p, double (&nz)[2]) {
             const Philox4 r = philox4x32_10(glo, ghi, (uint32_t)p, kTagNoise, C.seed_lo, C.seed_hi);
-            const double u1 = (double)(mc_u53(r.v[0], r.v[1]) + 1u) * 0x1p-53;  // (0, 1]
-            const double u2 = (double)mc_u53(r.v[2], r.v[3]) * 0x1p-53;         // [0, 1)
+            const double u1 = 2.0 - mc_one_m(r.v[0], r.v[1]);  // (0, 1]
+            const double u2 = mc_one_m(r.v[2], r.v[3]) - 1.0;  // [0, 1)
             const double rad = sqrt(-2.0 * mc_log(u1));
             double sn, cs;
             mc_sincos(6.283185307179586 * u2, &sn, &cs);
-            const double nz[2] = {rad * cs, rad * sn};
+            nz[0] = rad * cs;
+            nz[1] = rad * sn;
+        };
+        auto quantize = [&](int p, const double (&nz)[2]) {
             const uint32_t xbits = xw[(2 * p) >> 5] >> ((2 * p) & 31);
             int s_out[2];
 #pragma unroll
@@ -272,6 +293,14 @@ __global__ __launch_bounds__(64) void mc_frames_kernel(McChannel C, int64_t fram
                 *reinterpret_cast<uint16_t *>(sy + 2 * p) = (uint16_t)(s_out[0] | (s_out[1] << 8));
             else
                 *reinterpret_cast<int2 *>(sym_out + f * N + 2 * p) = make_int2(s_out[0], s_out[1]);
+        };
+        for (int p0 = 0; 2 * p0 < N; p0 += 128) {
+            const int pa = p0 + t, pb = p0 + 64 + t;
+            double na[2], nb[2];
+            noise(pa, na);
+            noise(pb, nb);
+            if (2 * pa < N) quantize(pa, na);
+            if (2 * pb < N) quantize(pb, nb);
         }
         __syncthreads();
         if (PRE) {
