@@ -48,6 +48,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+GUIDE_LDS_B32_GBS = 75000.0  # MI355X_MICROARCH.md §LDS: aggregate ds_read_b32, every CU streaming
+GUIDE_LDS_B64_GBS = 150000.0  # ... ds_read_b64 / b128
 LOOKUPS_PER_FRAME = 81920  # L*N*log2(N) LUT lookups at N=1024, L=8
 ONCHIP_BYTES_PER_LOOKUP = 4  # 2 operand symbols + 1 table byte + 1 result byte
 METRIC = "decoded frames/sec (N=1024, SCL-LUT L=8, Q=16) at 1/2/4/8 GPUs; BER match"
@@ -308,6 +310,12 @@ def roofline(args, dec, kt, frames, calls):
            "algorithmic_bytes_per_launch": onchip_per_frame * per_launch,
            "algorithmic": f"{onchip_per_frame} B/frame on-chip (SURVEY.md §8(d)) x {per_launch:.0f} frames per launch",
            "peak_probe": peaks, "lds_hit": kc.get("lds_hit"),
+           # the guide's aggregate LDS rates (MI355X_MICROARCH.md §LDS, every CU streaming) beside the probe:
+           # the lookups are ds_bpermute (a cross-lane crossbar read, ~40 % of ds_read_b32 when probed);
+           # LDS-resident tables read with ds_read_b32/_b64 measured 5 % slower (profiles/r03k_ab_lds_tables.txt)
+           "peak_guide": {"ds_read_b32": GUIDE_LDS_B32_GBS, "ds_read_b64": GUIDE_LDS_B64_GBS},
+           "frac_vs_guide_ds_read_b32": achieved / GUIDE_LDS_B32_GBS,
+           "traffic_bytes_per_frame": (kc.get("traffic") / per_launch) if kc.get("traffic") else None,
            "traffic_note": "HBM-side bytes per launch of this kernel, 2 x FETCH_SIZE + WRITE_SIZE from separate "
                            "rocprofv3 --pmc passes (profiles/counters.json via tools/counters.py)",
            "hbm": {"achieved": hbm_bytes / (call_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
