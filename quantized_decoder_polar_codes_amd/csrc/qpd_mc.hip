@@ -150,6 +150,9 @@ __device__ inline double mc_log(double u) {
     return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
 }
 
+#ifndef QPD_MC_PAIRS
+#define QPD_MC_PAIRS 1  // noise pairs per lane and round: 1 measured best (2: +1 %, 4: +5 % generator time; profiles/r03n_ab_generator_pairs.txt)
+#endif
 #ifndef QPD_MC_WPE
 #define QPD_MC_WPE 6  // 6 waves per SIMD: -2.5 % generator time vs 5 (profiles/r03j_ab_generator.txt)
 #endif
@@ -256,9 +259,9 @@ __global__ __launch_bounds__(64, QPD_MC_WPE) void mc_frames_kernel(McChannel C, 
                 if (!(w & sw)) xw[w] ^= xw[w + sw];
             __syncthreads();
         }
-        // AWGN + LLR + channel quantizer, positions 2p and 2p+1, two pairs per
-        // lane and round (p and p + 64): their Philox / log / sincos chains are
-        // independent straight-line code the scheduler interleaves
+        // AWGN + LLR + channel quantizer, positions 2p and 2p+1, QPD_MC_PAIRS
+        // pairs per lane and round (p, p + 64, ...): their Philox / log / sincos
+        // chains are independent straight-line code the scheduler interleaves
         auto noise = [&](int p, double (&nz)[2]) {
             const Philox4 r = philox4x32_10(glo, ghi, (uint32_t)p, kTagNoise, C.seed_lo, C.seed_hi);
             const double u1 = 2.0 - mc_one_m(r.v[0], r.v[1]);  // (0, 1]
@@ -294,13 +297,13 @@ __global__ __launch_bounds__(64, QPD_MC_WPE) void mc_frames_kernel(McChannel C, 
             else
                 *reinterpret_cast<int2 *>(sym_out + f * N + 2 * p) = make_int2(s_out[0], s_out[1]);
         };
-        for (int p0 = 0; 2 * p0 < N; p0 += 128) {
-            const int pa = p0 + t, pb = p0 + 64 + t;
-            double na[2], nb[2];
-            noise(pa, na);
-            noise(pb, nb);
-            if (2 * pa < N) quantize(pa, na);
-            if (2 * pb < N) quantize(pb, nb);
+        for (int p0 = 0; 2 * p0 < N; p0 += 64 * QPD_MC_PAIRS) {
+            double nz[QPD_MC_PAIRS][2];
+#pragma unroll
+            for (int i = 0; i < QPD_MC_PAIRS; ++i) noise(p0 + 64 * i + t, nz[i]);
+#pragma unroll
+            for (int i = 0; i < QPD_MC_PAIRS; ++i)
+                if (2 * (p0 + 64 * i + t) < N) quantize(p0 + 64 * i + t, nz[i]);
         }
         __syncthreads();
         if (PRE) {

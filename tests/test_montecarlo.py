@@ -238,7 +238,9 @@ def _pw_big(N, K):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,N,K,L,engine", [("SCL-LUT", 1024, 512, 8, "auto"), ("FastSCL-LUT", 1024, 512, 8, "auto"),
                                                ("SC-LUT", 128, 32, 1, "auto"), ("CA-SCL-LUT", 256, 124, 8, "auto"),
-                                               ("SCL-LUT", 256, 128, 4, "generic")])
+                                               ("SCL-LUT", 256, 128, 4, "generic"),
+                                               # output rows off the dword grid: the tail's byte path counts
+                                               ("SC-LUT", 128, 33, 1, "auto"), ("CA-SCL-LUT", 256, 126, 8, "auto")])
 def test_gpu_fused_generate_decode_equals_unfused(kind, N, K, L, engine, native_lib):
     """qpd_mc_decode (generation writes the decoder's root pre-pass rows on a
     fast-engine decoder, else its own symbol buffer) = qpd_mc_frames followed

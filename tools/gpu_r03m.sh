@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round 3 m: error counting in the decode kernel's tail on the fused Monte-Carlo
+# path (product) vs the separate count kernel (prev = the previous commit):
+# Monte-Carlo tests, then an interleaved A/B of the decode rate and the e2e rate.
+set -u
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_montecarlo.py -m gpu -q --timeout 120 --timeout-method thread > $O/r03m_pytest_mc.log 2>&1
+rc=$?; tail -3 $O/r03m_pytest_mc.log; [ $rc -eq 0 ] || exit $rc
+: > $O/r03m_ab.txt
+for round in 1 2; do
+  for kind in SCL-LUT FastSCL-LUT; do
+    for lib in prev prod; do
+      if [ $lib = prod ]; then unset QPD_LIB; else export QPD_LIB=build_variants/libqpd_$lib.so; fi
+      timeout -k 10 200 python bench.py --no-cpu-baseline --steps 4 --kind $kind > $O/r03m_tmp.log 2>&1 || exit $?
+      grep '^{' $O/r03m_tmp.log | python -c "import json,sys; r=json.loads(sys.stdin.read()); e=r['monte_carlo_e2e']; print('$round $lib $kind', round(r['value']/1e6,3), round(r['roofline']['kernel_ms'],3), round(e['value']/1e6,3), round(e['ms_per_step'],3))" | tee -a $O/r03m_ab.txt
+    done
+  done
+done
+echo done
