@@ -258,6 +258,7 @@ def run_rank(args, ctx, wl):
         res["config"].update({"engine": {1: "generic", 2: "fast"}[info["engine"]],
                               "lds_bytes_per_wave": info["lds_bytes_per_wave"],
                               "lds_from_depth": info["lds_from_depth"],
+                              "ops": info["num_ops"],
                               "waves": min(info["max_waves"], -(-frames // info["frames_per_wave"]))})
     if kt:
         res["roofline"] = roofline(args, dec, kt, frames, args.steps + args.warmup)
