@@ -336,32 +336,54 @@ __global__ __launch_bounds__(64, QPD_MC_WPE) void mc_frames_kernel(McChannel C, 
 
 // Bit and block errors of decoded frames against their messages, added to
 // counts[0] / counts[1] (the driver's counters, mainQuantizedDecoder_LLRDomain.py:181-183):
-// one wave per frame (grid-stride), 8 bytes per lane per step -- the bytes are
-// 0 / 1, so popcount(a ^ b) counts the differing ones -- two atomics per wave.
+// one wave per frame (grid-stride, four frames' loads in flight per wave), 8
+// bytes per lane per step -- the bytes are 0 / 1, so popcount(a ^ b) counts the
+// differing ones; a frame's block error is one ballot, the bit errors are
+// reduced once per wave; two atomics per wave.
 __global__ __launch_bounds__(256) void mc_count_kernel(const uint8_t *__restrict__ bits,
                                                        const uint8_t *__restrict__ msg, int64_t B, int K,
                                                        unsigned long long *__restrict__ counts) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
-    unsigned long long be = 0, fe = 0;
+    unsigned be = 0, fe = 0;  // be: this lane's share of the bit errors
     const bool vec = (K & 7) == 0 && ((uintptr_t)bits & 7) == 0 && ((uintptr_t)msg & 7) == 0;
-    for (int64_t f = wave; f < B; f += waves) {
-        const uint8_t *a = bits + f * K, *b = msg + f * K;
-        unsigned e = 0;
-        if (vec) {
-            for (int i = 8 * lane; i < K; i += 512)
-                e += __popcll(*(const unsigned long long *)(a + i) ^ *(const unsigned long long *)(b + i));
-        } else {
-            for (int i = lane; i < K; i += 64) e += (a[i] ^ b[i]) & 1u;
+    if (vec && K <= 512) {  // one 8-byte step per lane covers a frame
+        const bool on = 8 * lane < K;
+        for (int64_t f0 = wave; f0 < B; f0 += 4 * waves) {
+            unsigned long long x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t f = f0 + u * waves;
+                x[u] = 0;
+                if (f < B && on)
+                    x[u] = *(const unsigned long long *)(bits + f * K + 8 * lane) ^
+                           *(const unsigned long long *)(msg + f * K + 8 * lane);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                be += __popcll(x[u]);
+                fe += __ballot(x[u] != 0) != 0;
+            }
         }
-        for (int m = 32; m >= 1; m >>= 1) e += (unsigned)__shfl_xor((int)e, m, 64);
-        be += e;
-        fe += e != 0;
+    } else {
+        for (int64_t f = wave; f < B; f += waves) {
+            const uint8_t *a = bits + f * K, *b = msg + f * K;
+            unsigned e = 0;
+            if (vec) {
+                for (int i = 8 * lane; i < K; i += 512)
+                    e += __popcll(*(const unsigned long long *)(a + i) ^ *(const unsigned long long *)(b + i));
+            } else {
+                for (int i = lane; i < K; i += 64) e += (a[i] ^ b[i]) & 1u;
+            }
+            be += e;
+            fe += __ballot(e != 0) != 0;
+        }
     }
+    for (int m = 32; m >= 1; m >>= 1) be += (unsigned)__shfl_xor((int)be, m, 64);
     if (lane == 0 && be) {
-        atomicAdd(counts, be);
-        atomicAdd(counts + 1, fe);
+        atomicAdd(counts, (unsigned long long)be);
+        atomicAdd(counts + 1, (unsigned long long)fe);
     }
 }
 
