@@ -96,6 +96,16 @@ __device__ __host__ inline double mc_one_m(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(double, ((uint64_t)(0x3FF00000u | (a >> 12)) << 32) | b);
 }
 
+// One Horner step a * b + c with the constant c as an SGPR operand of a VOP3
+// v_fma_f64: the compiler otherwise keeps the polynomial constants in VGPRs and
+// evaluates every step as a copy + v_fmac_f64 (two VALU instructions instead
+// of one plus two scalar moves).
+__device__ __forceinline__ double hfma(double a, double b, double c) {
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
+}
+
 // sin and cos of x in [0, 2 pi] for the Box-Muller angle: reduction by
 // q = rint(x * 2/pi) against pi/2 in three parts (Cody-Waite), then the
 // fdlibm kernel polynomials (__kernel_sin / __kernel_cos, |r| <= pi/4, < 1 ulp).
@@ -107,13 +117,13 @@ __device__ inline void mc_sincos(double x, double *sn, double *cs) {
     r = fma(-q, 6.07710050630396597660e-11, r);
     r = fma(-q, 2.02226624879595063154e-21, r);
     const double z = r * r;
-    const double ps = fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
-                                         2.75573137070700676789e-06), -1.98412698298579493134e-04),
-                          8.33333333332248946124e-03);
-    const double sr = fma(r * z, fma(z, ps, -1.66666666666666324348e-01), r);
-    const double pc = z * fma(z, fma(z, fma(z, fma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
-                                                 -2.75573143513906633035e-07), 2.48015872894767294178e-05),
-                                      -1.38888888888741095749e-03), 4.16666666666666019037e-02);
+    const double ps = hfma(z, hfma(z, hfma(z, fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
+                                           2.75573137070700676789e-06), -1.98412698298579493134e-04),
+                           8.33333333332248946124e-03);
+    const double sr = fma(r * z, hfma(z, ps, -1.66666666666666324348e-01), r);
+    const double pc = z * hfma(z, hfma(z, hfma(z, hfma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+                                                      -2.75573143513906633035e-07), 2.48015872894767294178e-05),
+                                         -1.38888888888741095749e-03), 4.16666666666666019037e-02);
     const double hz = 0.5 * z, w = 1.0 - hz;
     const double cr = w + (((1.0 - w) - hz) + z * pc);
     // quadrant q & 3: (sr, cr), (cr, -sr), (-sr, -cr), (-cr, sr) -- as selects
@@ -143,9 +153,9 @@ __device__ inline double mc_log(double u) {
     s = fma(fma(-dd, s, f), r, s);
     const double z = s * s, w = z * z;
     // fdlibm's Horner steps as fused multiply-adds
-    const double t1 = w * fma(w, fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01), 3.999999999940941908e-01);
-    const double t2 = z * fma(w, fma(w, fma(w, 1.479819860511658591e-01, 1.818357216161805012e-01), 2.857142874366239149e-01),
-                              6.666666666666735130e-01);
+    const double t1 = w * hfma(w, fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01), 3.999999999940941908e-01);
+    const double t2 = z * hfma(w, hfma(w, fma(w, 1.479819860511658591e-01, 1.818357216161805012e-01), 2.857142874366239149e-01),
+                               6.666666666666735130e-01);
     const double R = t2 + t1, hfsq = 0.5 * f * f, dk = (double)k;
     return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
 }
