@@ -40,17 +40,40 @@ __device__ __forceinline__ uint64_t ptr_set(uint64_t p, int d, int lane_in_group
     return (p & ~m) | ((uint64_t)lane_in_group << (4 * d));
 }
 
-__device__ __forceinline__ uint64_t shfl64(uint64_t x, int src) {
-    uint32_t lo = __shfl((uint32_t)x, src);
-    uint32_t hi = __shfl((uint32_t)(x >> 32), src);
+// Lane `src` (0..63, taken mod 64) of x: one ds_bpermute at byte address
+// src * 4.  HIP's __shfl computes the same read but first rebuilds the lane id
+// (two mbcnt) and re-bases the source on it; the wave is 64 wide, so there is
+// nothing to re-base (SCL-LUT +0.7 %, profiles/r03t_ab_lane_read.txt).  The
+// FastSCL-LUT unit (qpd_fast_fscl.hip) keeps __shfl (QPD_LANE_READ_SHFL): there
+// the change moves its register allocation and costs 12 %.  Internal linkage,
+// so the two units' definitions stay separate.
+#ifdef QPD_LANE_READ_SHFL
+static __device__ __forceinline__ uint32_t lane_read(uint32_t x, int src) { return __shfl(x, src); }
+static __device__ __forceinline__ int lane_read(int x, int src) { return __shfl(x, src); }
+#else
+static __device__ __forceinline__ uint32_t lane_read(uint32_t x, int src) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)x);
+}
+static __device__ __forceinline__ int lane_read(int x, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, x); }
+#endif
+
+static __device__ __forceinline__ uint64_t shfl64(uint64_t x, int src) {
+    const uint32_t lo = lane_read((uint32_t)x, src);
+    const uint32_t hi = lane_read((uint32_t)(x >> 32), src);
     return ((uint64_t)hi << 32) | lo;
 }
 
-__device__ __forceinline__ double shfld(double x, int src) { return __shfl(x, src); }
+#ifdef QPD_LANE_READ_SHFL
+static __device__ __forceinline__ double shfld(double x, int src) { return __shfl(x, src); }
+#else
+static __device__ __forceinline__ double shfld(double x, int src) {
+    return __builtin_bit_cast(double, shfl64(__builtin_bit_cast(uint64_t, x), src));
+}
+#endif
 
 // Cross-lane reads (ds_bpermute) see 0 from lanes that are inactive for the
 // instruction, so every shuffle runs with the whole wave active: evaluate both
-// sides first, then select (never `c ? __shfl(a) : __shfl(b)`).
+// sides first, then select (never `c ? lane_read(a) : lane_read(b)`).
 __device__ __forceinline__ double pick(bool c, double a, double b) { return c ? a : b; }
 
 __device__ __forceinline__ void wave_sync() { __syncthreads(); }  // 64-thread block: one wave
@@ -220,7 +243,7 @@ __device__ __forceinline__ int ca_winner_ranked(int rank, int gl, int gbase, int
     const int key = gl < L ? (pass ? rank : kMaxLWide + rank) : 2 * kMaxLWide;
     int best = 0, bk = 1 << 30;
     for (int j = 0; j < L; ++j) {
-        const int kj = __shfl(key, gbase + j);
+        const int kj = lane_read(key, gbase + j);
         if (kj < bk) {
             bk = kj;
             best = j;

@@ -478,12 +478,12 @@ __device__ __forceinline__ uint32_t leaf_fork(Path &st, double dm, int gl, int g
         if (keep_all8(__builtin_bit_cast(uint64_t, st.pm), __builtin_bit_cast(uint64_t, kf), gl)) return hd;
     const Sel sl = L8 ? select_survivors8(st.pm, kf, gl, gbase, lane, sel) : select_survivors(st.pm, kf, gl, gbase, L, sel);
     const int p = gbase + sl.parent;
-    const uint32_t dec = (uint32_t)__shfl((int)hd, p) ^ (sl.upper ? 1u : 0u);
+    const uint32_t dec = (uint32_t)lane_read((int)hd, p) ^ (sl.upper ? 1u : 0u);
     st.pm = pick(sl.upper, shfld(kf, p), shfld(st.pm, p));
     st.ps = shfl64(st.ps, p);
     st.pu = shfl64(st.pu, p);
 #pragma unroll
-    for (int i = 0; i < NX; ++i) extra[i] = (uint32_t)__shfl((int)extra[i], p);
+    for (int i = 0; i < NX; ++i) extra[i] = (uint32_t)lane_read((int)extra[i], p);
     return dec;
 }
 
@@ -681,18 +681,18 @@ __device__ __forceinline__ uint32_t r1_layers(Path &st, int *sel, int gl, int gb
             // the identity too, so the node is decided.
             if constexpr (L8)
                 if (keep_all8(__builtin_bit_cast(uint64_t, st.pm), __builtin_bit_cast(uint64_t, kf), gl)) break;
-            const int pos_old = __shfl(own, o);  // H2
+            const int pos_old = lane_read(own, o);  // H2
             const Sel sl = L8 ? select_survivors8(st.pm, kf, gl, gbase, lane, sel)
                               : select_survivors(st.pm, kf, gl, gbase, L, sel);
             const int p = gbase + sl.parent;
             st.pm = pick(sl.upper, shfld(kf, p), shfld(st.pm, p));
             st.ps = shfl64(st.ps, p);
             st.pu = shfl64(st.pu, p);
-            origin = __shfl(origin, p);
-            flips = (uint32_t)__shfl((int)flips, p) ^ (sl.upper ? 1u << (pos_old & 31) : 0u);
+            origin = lane_read(origin, p);
+            flips = (uint32_t)lane_read((int)flips, p) ^ (sl.upper ? 1u << (pos_old & 31) : 0u);
         }
     }
-    const uint32_t word = (uint32_t)__shfl((int)hw, gbase + origin) ^ flips;
+    const uint32_t word = (uint32_t)lane_read((int)hw, gbase + origin) ^ flips;
     return temp < 32 ? word & ((1u << temp) - 1u) : word;
 }
 
@@ -711,7 +711,7 @@ __device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const 
     const uint32_t rrow = uni && s16 < v ? (uint32_t)rk[s16] : 0u;
     const double vrow = uni && s16 < v ? vq[s16] : 0.0;
     auto rank_of = [&](int j, uint32_t sym) -> uint32_t {
-        return uni ? (uint32_t)__shfl((int)rrow, (int)sym) : (uint32_t)rk[j * v + sym];
+        return uni ? (uint32_t)lane_read((int)rrow, (int)sym) : (uint32_t)rk[j * v + sym];
     };
     uint32_t W[4], hw = 0;
 #pragma unroll
@@ -844,11 +844,11 @@ __device__ __forceinline__ void r1_large(const FastPlan &P, const Mem &M, const 
             st.pm = pick(sx.upper, shfld(kf, p), shfld(st.pm, p));
             st.ps = shfl64(st.ps, p);
             st.pu = shfl64(st.pu, p);
-            origin = __shfl(origin, p);
+            origin = lane_read(origin, p);
             for (int q = 0; q < kMaxM; ++q) {
-                ord[q] = __shfl(ord[q], p);
+                ord[q] = lane_read(ord[q], p);
                 ms[q] = shfld(ms[q], p);
-                if (q < layer) flip[q] = __shfl(flip[q], p);
+                if (q < layer) flip[q] = lane_read(flip[q], p);
             }
             flip[layer] = sx.upper ? pos_old : -1;
         }
@@ -1319,7 +1319,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
 #pragma unroll
                     for (int k = 0; k < 8; ++k)
                         if (k < wpl) {
-                            const uint32_t o = (uint32_t)__shfl((int)x[k], lane ^ lm);
+                            const uint32_t o = (uint32_t)lane_read((int)x[k], lane ^ lm);
                             if (!(gl & lm)) x[k] ^= o;
                         }
 #pragma unroll

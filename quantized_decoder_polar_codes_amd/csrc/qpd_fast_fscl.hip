@@ -6,6 +6,7 @@
 // so only FastSCL takes it.  Diagnostic builds that read device globals
 // (QPD_STAMPS) keep every instantiation in qpd_capi.hip instead.
 #define QPD_FAST_TEMPLATES_ONLY
+#define QPD_LANE_READ_SHFL  // HIP's __shfl for the shuffles (see lane_read, qpd_common.hpp)
 #include "qpd_fast.hip"
 
 namespace qpd {
