@@ -11,7 +11,7 @@ mkdir -p "$OUT/obj_$NAME"
 SRC="${QPD_VARIANT_SRC:-$ROOT/quantized_decoder_polar_codes_amd/csrc}"  # another tree: QPD_VARIANT_SRC=DIR/csrc
 CXX="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I${QPD_VARIANT_INC:-$ROOT/include} -I$SRC $*"
 $CXX -c "$SRC/qpd_capi.hip" -o "$OUT/obj_$NAME/capi.o" -Rpass-analysis=kernel-resource-usage > "$OUT/obj_$NAME/capi.log" 2>&1 &
-$CXX -mllvm -amdgpu-sched-strategy=max-ilp -c "$SRC/qpd_fast_fscl.hip" -o "$OUT/obj_$NAME/fscl.o" -Rpass-analysis=kernel-resource-usage > "$OUT/obj_$NAME/fscl.log" 2>&1 &
+$CXX -mllvm -amdgpu-sched-strategy=${FSCL_SCHED:-max-ilp} -c "$SRC/qpd_fast_fscl.hip" -o "$OUT/obj_$NAME/fscl.o" -Rpass-analysis=kernel-resource-usage > "$OUT/obj_$NAME/fscl.log" 2>&1 &
 $CXX -c "$SRC/qpd_lutgen.cpp" -o "$OUT/obj_$NAME/lutgen.o" > "$OUT/obj_$NAME/lutgen.log" 2>&1 &
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$OUT/obj_$NAME/capi.o" "$OUT/obj_$NAME/fscl.o" "$OUT/obj_$NAME/lutgen.o" -o "$OUT/libqpd_$NAME.so"
