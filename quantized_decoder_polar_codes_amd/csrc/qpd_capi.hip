@@ -601,7 +601,10 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
         L.lds_base[n + 1] = rl;
         L.lds_end = rl + qpd::kSelInts / 64;
     };
-    d->sets = c->kind == QPD_FASTSCL_LUT ? 1 : kDefaultSets;  // FastSCL's R1 argsort state spills at NS = 2
+    // one frame set for the Fast kinds: their special nodes' state spills at NS = 2
+    // (FastSCL's R1 argsort; FastSC-LUT N=1024: 171 -> 241 M frames/s with one set,
+    // profiles/r03z_sets.txt)
+    d->sets = (c->kind == QPD_FASTSCL_LUT || c->kind == QPD_FASTSC_LUT) ? 1 : kDefaultSets;
     if (const char *e = getenv("QPD_SETS")) d->sets = std::min(2, std::max(1, atoi(e)));
 #ifdef QPD_SETS3
     if (const char *e = getenv("QPD_SETS")) if (atoi(e) == 3 && c->kind == QPD_SCL_LUT && d->L == 8) d->sets = 3;
