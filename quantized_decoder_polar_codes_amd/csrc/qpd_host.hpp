@@ -559,6 +559,9 @@ class Engine {
                 key[i] = pm[i];
                 key[L + i] = pm[i] + r1_a[o * st + pos_old[i]];
             }
+#ifdef QPD_HOST_R1_HOOK
+            QPD_HOST_R1_HOOK(key.data(), L, layer, m, temp);  // diagnostic builds: R1 layer statistics
+#endif
             select();
             for (int i = 0; i < L; ++i) {
                 const int c = idx[i], par = c % L;
