@@ -258,7 +258,7 @@ def run_rank(args, ctx, wl):
         res["config"].update({"engine": {1: "generic", 2: "fast"}[info["engine"]],
                               "lds_bytes_per_wave": info["lds_bytes_per_wave"],
                               "lds_from_depth": info["lds_from_depth"],
-                              "ops": info["num_ops"],
+                              "ops": info["num_ops"], "prefix_ops": info.get("prefix_ops", 0),
                               "waves": min(info["max_waves"], -(-frames // info["frames_per_wave"]))})
     if kt:
         res["roofline"] = roofline(args, dec, kt, frames, args.steps + args.warmup)
@@ -289,8 +289,10 @@ def roofline(args, dec, kt, frames, calls):
 
     dec_ms, n_dec = kt["decode"]
     pre_ms, n_pre = kt["pre"]
-    k_ms = dec_ms / max(1, n_dec)
-    call_ms = (dec_ms + pre_ms) / max(1, calls)
+    pfx_ms, n_pfx = kt.get("pfx", (0.0, 0))
+    # the decode of a launch's frames = lut_prefix_kernel (frozen prefix, list kinds) + lut_fast_kernel
+    k_ms = (dec_ms + pfx_ms) / max(1, n_dec)
+    call_ms = (dec_ms + pre_ms + pfx_ms) / max(1, calls)
     per_launch = frames * calls / max(1, n_dec)  # frames per decode launch
     n = int(np.log2(args.N))
     onchip_per_frame = args.L * args.N * n * ONCHIP_BYTES_PER_LOOKUP if "SCL" in args.kind else args.N * n * 4
@@ -307,7 +309,9 @@ def roofline(args, dec, kt, frames, calls):
     kname = "lut_fast_kernel" if dec.info()["engine"] == 2 else "generic_decode_kernel"
     kc = (rec or {}).get("kernels", {}).get(kname, {})
     out = {"bound": "lds", "achieved": achieved, "peak": peak, "unit": "GB/s", "frac": achieved / peak,
-           "traffic": kc.get("traffic"), "kernel": kname, "kernel_ms": k_ms, "launches": n_dec,
+           "traffic": kc.get("traffic"), "kernel": kname, "kernel_ms": dec_ms / max(1, n_dec), "launches": n_dec,
+           "prefix_kernel_ms": pfx_ms / max(1, n_pfx) if n_pfx else None,
+           "achieved_over": "lut_fast_kernel + lut_prefix_kernel per launch" if n_pfx else kname,
            "algorithmic_bytes_per_launch": onchip_per_frame * per_launch,
            "algorithmic": f"{onchip_per_frame} B/frame on-chip (SURVEY.md §8(d)) x {per_launch:.0f} frames per launch",
            "peak_probe": peaks, "lds_hit": kc.get("lds_hit"),

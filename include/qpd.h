@@ -293,6 +293,9 @@ typedef struct qpd_info {
     int32_t out_bits;         /* bits per decoded frame: K, or A (CRC-aided)  */
     int64_t host_max_frames;  /* host-buffer calls of up to this many frames run
                                  on the host engine (qpd_set_host_engine); 0: none */
+    int32_t prefix_ops;       /* fast engine, list kinds: ops of the frozen prefix run
+                                 once per frame by lut_prefix_kernel (0: no split);
+                                 num_ops counts both parts */
 } qpd_info;
 int qpd_get_info(const qpd_decoder *dec, qpd_info *info);
 
@@ -307,7 +310,8 @@ enum qpd_kernel_class {
     QPD_KC_PRE = 0,    /* root_pre_kernel (fast engine, root pre-pass)              */
     QPD_KC_DECODE = 1, /* lut_fast_kernel / generic_decode_kernel                   */
     QPD_KC_MC = 2,     /* mc_frames_kernel (qpd_mc_frames)                          */
-    QPD_KC_COUNT = 3
+    QPD_KC_PFX = 3,    /* lut_prefix_kernel (fast engine, frozen prefix of list kinds) */
+    QPD_KC_COUNT = 4
 };
 int qpd_profile(qpd_decoder *dec, int32_t enable);
 int qpd_kernel_times(qpd_decoder *dec, double *ms, int64_t *launches);

@@ -43,7 +43,7 @@ EXPORTED = (
     "qpd_probe_lds",
     "qpd_set_host_engine",
 )
-QPD_KC_PRE, QPD_KC_DECODE, QPD_KC_MC, QPD_KC_COUNT = range(4)
+QPD_KC_PRE, QPD_KC_DECODE, QPD_KC_MC, QPD_KC_PFX, QPD_KC_COUNT = range(5)
 QPD_PROBE_BPERMUTE, QPD_PROBE_READ_B32, QPD_PROBE_READ_B64 = range(3)
 QPD_HOST_AUTO, QPD_HOST_GPU, QPD_HOST_CPU = range(3)
 
@@ -118,6 +118,7 @@ class QpdInfo(ctypes.Structure):
         ("lds_from_depth", _i32),
         ("out_bits", _i32),
         ("host_max_frames", _i64),
+        ("prefix_ops", _i32),
     ]
 
 

@@ -89,6 +89,8 @@ struct qpd_decoder {
     qpd::FastPlan fplan{};
     DeviceBuf f_tab, g_tab, fscratch, mops, r1_rank, task_ctr;
     int num_mops = 0;
+    DeviceBuf pfx_mops;  // frozen-prefix ops (lut_prefix_kernel); empty: no split
+    int pfx_nops = 0;
     std::vector<Op> ops_host;
     DeviceBuf lut_f, f_base, lut_g, g_base, vcl, ops, info_pos, scratch, err;
     DeviceBuf r_f, r_g, q_bnd, q_rec, bnd_off, bnd_len, rec_off, rec_len;  // float-domain re-quantizers
@@ -505,6 +507,147 @@ void place_syncs(std::vector<qpd::MOp> &ops, bool list) {
     }
 }
 
+// Row ownership of a fast layout: (space, row) -> slot, for the prefix split.
+struct FastOwner {
+    std::vector<int8_t> kind[2];  // per space (0 slab, 1 LDS): -1 unowned, 0 U/R row, 1 S row
+    void add(bool lds, int base, int cnt, bool srow) {
+        auto &k = kind[lds ? 1 : 0];
+        if ((int)k.size() < base + cnt) k.resize(base + cnt, -1);
+        for (int r = 0; r < cnt; ++r) k[base + r] = srow ? 1 : 0;
+    }
+    int of(int sp, int row) const { return row >= 0 && row < (int)kind[sp].size() ? kind[sp][row] : -1; }
+};
+
+// Rows of the fast engine's slab / LDS an op reads and writes (space, first
+// row, count), from the access pattern of its code in qpd_fast.hip.  Reads of
+// the channel or a pre-pass row (MF_CHAN / MF_PRE) are not row reads.
+template <class Fn>
+void op_rows(const qpd::MOp &m, Fn &&acc) {
+    using namespace qpd;
+    const int fl = m.flags;
+    const bool src_row = !(fl & (MF_CHAN | MF_PRE));
+    const int sp_s = (fl & MF_SRC_LDS) ? 1 : 0, sp_u = (fl & MF_U_LDS) ? 1 : 0, sp_d = (fl & MF_DST_LDS) ? 1 : 0;
+    const int c = m.cnt;
+    switch (m.type) {
+        case OP_F:
+        case OP_G:
+            if (src_row) acc(false, sp_s, m.src_row, c >= 8 ? 2 * (c >> 3) : 1);
+            if (m.type == OP_G) acc(false, sp_u, m.u_row, std::max(1, c >> 5));
+            acc(true, sp_d, m.dst_row, c >= 8 ? c >> 3 : 1);
+            break;
+        case OP_COMB: {
+            const int cw = c < 32 ? 1 : c >> 5;
+            acc(false, sp_u, m.u_row, cw);
+            acc(false, (fl & MF_R_LDS) ? 1 : 0, m.r_row, cw);
+            acc(true, sp_d, m.dst_row, c < 32 ? 1 : 2 * cw);
+            break;
+        }
+        case OP_LEAF_L:
+        case OP_LEAF_R:
+            if (src_row) acc(false, sp_s, m.src_row, 1);
+            if (m.type == OP_LEAF_R) acc(false, sp_u, m.u_row, 1);
+            acc(true, sp_d, m.dst_row, 1);
+            break;
+        case OP_BOT3:
+            if (src_row) acc(false, sp_s, m.src_row, (fl & MF_BFG) ? 2 : 1);
+            if (fl & (MF_BG | MF_BCOMB)) acc(false, sp_u, m.u_row, 1);
+            acc(true, sp_d, m.dst_row, 1);
+            break;
+        case OP_IMPORT: acc(true, sp_d, m.dst_row, c); break;
+        case OP_EXPORT: acc(false, sp_s, m.src_row, c); break;
+        default:  // special nodes: temp symbols in, temp bits out
+            acc(false, sp_s, m.src_row, (c + 7) >> 3);
+            acc(true, sp_d, m.dst_row, (c + 31) >> 5);
+            break;
+    }
+}
+
+// Split a list decoder's schedule at its first forking op (see
+// lut_prefix_kernel): `pfx` = the ops before it + OP_EXPORT of every S row
+// word the rest reads before writing; `rest` = OP_IMPORT of those words (from
+// the pre-pass row) and zeros for the U / R words (every prefix decision is a
+// frozen 0) + the ops from the fork on.  False (no split) when there is no
+// prefix, the live rows are not S / U / R rows, or they do not fit the free
+// quarter of the pre-pass row next to the metric.
+bool split_prefix(const std::vector<qpd::MOp> &ops, const FastOwner &own, int N, std::vector<qpd::MOp> &pfx,
+                  std::vector<qpd::MOp> &rest) {
+    using namespace qpd;
+    size_t s = 0;
+    for (; s < ops.size(); ++s) {
+        const MOp &m = ops[s];
+        const bool forks = (m.type == OP_BOT3 && m.cnt != 0xff) || ((m.type == OP_LEAF_L || m.type == OP_LEAF_R) && m.cnt == 0) ||
+                           m.type == OP_R1 || m.type == OP_REP || m.type == OP_SPC;
+        if (forks) break;
+    }
+    if (s == 0 || s == ops.size()) return false;
+    // live-in words of the rest: read before any op of the rest writes them
+    std::vector<char> def[2], live[2];
+    for (int sp = 0; sp < 2; ++sp) {
+        def[sp].assign(own.kind[sp].size() + 1, 0);
+        live[sp].assign(own.kind[sp].size() + 1, 0);
+    }
+    bool ok = true;
+    for (size_t i = s; i < ops.size() && ok; ++i) {
+        op_rows(ops[i], [&](bool wr, int sp, int row, int cnt) {
+            for (int r = row; r < row + cnt; ++r) {
+                if (own.of(sp, r) < 0) {
+                    if (!wr) ok = false;  // an unowned row read (scratch): no split
+                    continue;
+                }
+                if (wr) def[sp][r] = 1;
+                else if (!def[sp][r]) live[sp][r] = 1;
+            }
+        });
+    }
+    if (!ok) return false;
+    const int q0 = 3 * (N / 16), pm_off = N / 4 - 2;  // free quarter: [q0, pm_off) rows, then the metric
+    int at = q0;
+    std::vector<MOp> imp, exp;
+    for (int sp = 0; sp < 2; ++sp)
+        for (int r = 0; r < (int)own.kind[sp].size();) {
+            if (!live[sp][r]) {
+                ++r;
+                continue;
+            }
+            const int k = own.of(sp, r);
+            int e = r;
+            while (e < (int)own.kind[sp].size() && live[sp][e] && own.of(sp, e) == k) ++e;
+            MOp m;
+            std::memset(&m, 0, sizeof(m));
+            m.type = OP_IMPORT;
+            m.dst_row = r;
+            m.cnt = e - r;
+            m.flags = sp ? MF_DST_LDS : 0;
+            if (k == 1) {  // S row words: computed by the prefix
+                if (at + m.cnt > pm_off) return false;
+                m.flags |= MF_PRE;
+                m.src_row = at;
+                MOp x = m;
+                x.type = OP_EXPORT;
+                x.flags = sp ? MF_SRC_LDS : 0;
+                x.src_row = r;
+                x.dst_row = at;
+                exp.push_back(x);
+                at += m.cnt;
+            } else {
+                m.flags |= MF_ZERO;
+            }
+            imp.push_back(m);
+            r = e;
+        }
+    MOp pm;  // path 0's metric
+    std::memset(&pm, 0, sizeof(pm));
+    pm.type = OP_IMPORT;
+    pm.flags = MF_PRE | MF_PM;
+    pm.src_row = pm_off;
+    imp.insert(imp.begin(), pm);
+    pfx.assign(ops.begin(), ops.begin() + s);
+    pfx.insert(pfx.end(), exp.begin(), exp.end());
+    rest = imp;
+    rest.insert(rest.end(), ops.begin() + s, ops.end());
+    return true;
+}
+
 #ifndef QPD_DEFAULT_SETS
 #define QPD_DEFAULT_SETS 2
 #endif
@@ -539,6 +682,14 @@ const void *fast_kernel(int kind, int sets, bool l8, bool r1l) {
     }
 #undef QPD_FKR
 #undef QPD_FK
+}
+
+const void *prefix_kernel(int kind) {
+    using namespace qpd;
+    switch (kind) {
+        case QPD_SCL_LUT: return reinterpret_cast<const void *>(&lut_prefix_kernel(K_SCL_LUT));
+        default: return nullptr;
+    }
 }
 
 // Task queue of the persistent kernels: one counter, never reset (wave_take).
@@ -687,12 +838,37 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
         if (rc) return rc;
     }
     F.r1_rank = (const uint16_t *)d->r1_rank.p;
+    // Frozen-prefix split (lut_prefix_kernel): list kinds in pre-mode.
+    std::vector<qpd::MOp> pfx;
+    F.pm_off = -1;
+    // SCL-LUT only: FastSCL's R0 / REP nodes already take most of the prefix (4 ops of the
+    // bench code; the split measured -3 %, profiles/r03ab_*)
+    if (Ly.pre && d->L > 1 && c->kind == QPD_SCL_LUT && !getenv("QPD_NO_PFX")) {
+        FastOwner own;
+        for (int dd = 0; dd <= n; ++dd)
+            for (int sl = 0; sl < 3; ++sl) {
+                const int b = sl == 0 ? Ly.R[dd] : sl == 1 ? Ly.S[dd] : Ly.U[dd];
+                const int cnt = use[sl][dd] ? rows_of(sl, dd) : 0;
+                own.add(Ly.lds(dd), b, cnt, sl == 1);
+            }
+        std::vector<qpd::MOp> rest;
+        if (split_prefix(mops, own, N, pfx, rest)) {
+            mops.swap(rest);
+            F.pm_off = N / 4 - 2;  // the prefix kernel's metric word (split_prefix)
+        }
+    }
+    place_syncs(pfx, true);
     place_syncs(mops, c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT);
+    d->pfx_nops = (int)pfx.size();
+    if (!pfx.empty()) {
+        int rc = upload(d->pfx_mops, pfx.data(), pfx.size(), d->hs);
+        if (rc) return rc;
+    }
     for (const qpd::MOp &m : mops)  // R1 nodes the register/LDS argsort cannot take
         if (c->kind == QPD_FASTSCL_LUT && m.type == qpd::OP_R1 && m.cnt > qpd::stl::kThreshold && !(m.flags & qpd::MF_R1_LDS))
             d->r1l = true;
     F.nops = (int)mops.size();
-    d->num_mops = F.nops;
+    d->num_mops = F.nops + d->pfx_nops;
     {
         int rc = upload(d->mops, mops.data(), mops.size(), d->hs);
         if (rc) return rc;
@@ -1084,6 +1260,7 @@ int qpd_get_info(const qpd_decoder *d, qpd_info *info) {
     info->engine = d->engine;
     info->lds_bytes_per_wave = d->lds_bytes;
     info->lds_from_depth = d->engine == QPD_ENGINE_FAST ? d->fplan.lds_from : -1;
+    info->prefix_ops = d->engine == QPD_ENGINE_FAST ? d->pfx_nops : 0;
     return QPD_OK;
 }
 
@@ -1095,9 +1272,10 @@ namespace {
 // stream ordered).
 // One fast-engine decode launch over Bc frames whose rows start at `in`
 // (channel symbols, in_shift = n; or pre-pass rows, in_shift = n - 2).
-int fast_launch(qpd_decoder *d, qpd::FastPlan fp, const int32_t *in, int64_t Bc, uint8_t *out, hipStream_t st) {
-    const int64_t tw = (int64_t)d->fplan.fpw * d->sets;  // frames per wave task
-    const void *kfn = fast_kernel(d->kind, d->sets, d->l8, d->r1l);
+int fast_launch(qpd_decoder *d, qpd::FastPlan fp, const int32_t *in, int64_t Bc, uint8_t *out, hipStream_t st,
+                bool prefix = false) {
+    const int64_t tw = (int64_t)fp.fpw * (prefix ? 1 : d->sets);  // frames per wave task
+    const void *kfn = prefix ? prefix_kernel(d->kind) : fast_kernel(d->kind, d->sets, d->l8, d->r1l);
     if (!kfn) return fail(QPD_E_INVALID, "bad kind");
     const int64_t fgroups = (Bc + tw - 1) / tw;
     int fgrid = (int)std::min<int64_t>(fgroups, d->max_waves);
@@ -1109,8 +1287,9 @@ int fast_launch(qpd_decoder *d, qpd::FastPlan fp, const int32_t *in, int64_t Bc,
     const qpd::MOp *ops_arg = fp.ops;
     fp.task_base = d->task_base;
     void *args[] = {&fp, &in, &Bc, &out, &ops_arg};
-    const size_t lds = (size_t)d->lds_bytes;
-    const int rc = timed_launch(d, QPD_KC_DECODE, st, [&]() -> int {
+    // the prefix kernel runs one frame set per wave in the same per-set layout
+    const size_t lds = (size_t)(prefix ? d->lds_bytes / d->sets : d->lds_bytes);
+    const int rc = timed_launch(d, prefix ? QPD_KC_PFX : QPD_KC_DECODE, st, [&]() -> int {
         QPD_HIP(hipLaunchKernel(kfn, dim3(fgrid), dim3(64), args, lds, st));
         QPD_HIP(hipGetLastError());
         return QPD_OK;
@@ -1124,6 +1303,17 @@ int decode_pre_rows(qpd_decoder *d, const uint32_t *rows, int64_t Bc, uint8_t *o
     qpd::FastPlan fp = d->fplan;
     fp.in_vec = 1;
     fp.in_shift = fp.n - 2;
+    if (d->pfx_nops > 0) {  // the frozen prefix once per frame, into the rows' free quarter
+        qpd::FastPlan pp = fp;
+        pp.ops = (const qpd::MOp *)d->pfx_mops.p;
+        pp.nops = d->pfx_nops;
+        pp.gs = 1;
+        pp.fpw = 64;
+        pp.L = 1;
+        pp.pfx = const_cast<uint32_t *>(rows);
+        const int rc = fast_launch(d, pp, (const int32_t *)rows, Bc, nullptr, st, true);
+        if (rc) return rc;
+    }
     return fast_launch(d, fp, (const int32_t *)rows, Bc, out, st);
 }
 

@@ -30,7 +30,9 @@
 
 namespace qpd {
 
-constexpr int OP_BOT3 = 9;  // fused bottom subtree of height 3 (fast engine only)
+constexpr int OP_BOT3 = 9;    // fused bottom subtree of height 3 (fast engine only)
+constexpr int OP_IMPORT = 10; // frozen-prefix split (see lut_prefix_kernel): rows from the pre-pass row / zeros
+constexpr int OP_EXPORT = 11; // lut_prefix_kernel only: rows into the pre-pass row's free quarter
 
 enum MopFlag : int32_t {
     MF_SRC_LDS = 1,   // S[d] in LDS
@@ -49,6 +51,8 @@ enum MopFlag : int32_t {
     MF_BCOMB = 4096,  // right BOT3 that also runs its parent's combine (dst = U/R[n-4])
     MF_VUNI = 8192,   // special node whose elements share one quanta row (v <= 16): quanta and
                       //   R1 ranks are looked up in a register row instead of gathered per element
+    MF_ZERO = 16384,  // OP_IMPORT: zero rows (partial sums of the frozen prefix) instead of pre-row words
+    MF_PM = 32768,    // OP_IMPORT: path 0's metric (a double at word src_row of the pre-pass row)
 };
 
 struct MOp {
@@ -89,6 +93,10 @@ struct FastPlan {
     int32_t *err;
     uint32_t *task_ctr;           // QPD_DYN task queue: tasks taken (never reset; see wave_take)
     uint32_t task_base;           // per launch: the counter's value when this launch's takes begin
+    // lut_prefix_kernel: the pre-pass rows, writable (the prefix's live rows and path
+    // metric go to the free last quarter of each frame's row; the metric at pm_off)
+    uint32_t *pfx;
+    int32_t pm_off;
 };
 
 // Timing experiments only (wrong results): 0 = every op reads node 0's
@@ -1021,10 +1029,15 @@ __device__ unsigned long long qpd_stamp_acc[64];
 // NS frame sets per wave (see above); L8: list decoders with L = 8.
 // LDS: NS * kSelInts ints of selection scratch, then NS * lds_rows rows.
 // Global slab: NS * glb_rows rows per workgroup.
-template <int KIND, int NS, bool L8, bool R1L = false>
+// PFX: the frozen-prefix kernel (lut_prefix_kernel below; one set, gs = 1, no
+// tail, `out` unused).  A template argument rather than a wrapper around a
+// shared body: the wrapper moved the decode kernels' register allocation
+// (FastSCL-LUT 63 -> 71 ms per 2^21 frames, profiles/r03ac_ab.txt).
+//
 // `ops` is its own __restrict__ argument (= P.ops) so that the compiler can
 // prove the op records are never written and fetch them with scalar loads
 // instead of vector loads + readfirstlane, which drain vmcnt at every op.
+template <int KIND, int NS, bool L8, bool R1L = false, bool PFX = false>
 __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QPD_WPE_FSCL : QPD_WPE1) void lut_fast_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
                                                                uint8_t *__restrict__ out,
                                                                const MOp *__restrict__ ops) {
@@ -1224,6 +1237,30 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
                     }
                     break;
                 }
+                case OP_IMPORT:
+                    if constexpr (KIND == K_SCL_LUT && !PFX) {  // the frozen prefix's results (lut_prefix_kernel)
+                        if (fl & MF_PM) {  // path 0 resumes from the prefix's metric
+#pragma unroll
+                            for (int s = 0; s < NS; ++s)
+                                stv[s].pm = gl == 0 ? *(const double *)(yv[s] + op.src_row) : kInf;
+                        } else {  // its live rows, into every path's own column
+                            const bool dl = fl & MF_DST_LDS, z = fl & MF_ZERO;
+#pragma unroll
+                            for (int s = 0; s < NS; ++s)
+                                for (int w = 0; w < op.cnt; ++w)
+                                    Mv[s].st(dl, op.dst_row + w, lane, z ? 0u : ((const uint32_t *)yv[s])[op.src_row + w]);
+                        }
+                    }
+                    break;
+                case OP_EXPORT:
+                    if constexpr (KIND == K_SCL_LUT && PFX) {  // one frame per lane (gs = 1, one set)
+                        const int64_t f = task * fpw + lane;
+                        for (int w = 0; w < op.cnt; ++w) {
+                            const uint32_t x = Mv[0].ld(fl & MF_SRC_LDS, op.src_row + w, lane);
+                            if (f < B) P.pfx[(f << P.in_shift) + op.dst_row + w] = x;
+                        }
+                    }
+                    break;
                 default: if constexpr (KIND == K_FASTSC_LUT || KIND == K_FASTSCL_LUT) {  // special nodes, FastSCLUT.cpp:46-107 / FastSCLLUTDecoder.cpp:82-213
                   for (int s = 0; s < NS; ++s) {
                     Path &st = stv[s];
@@ -1250,6 +1287,12 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
                 if ((int)(threadIdx.x & 31) == cls) stamp_cnt += 1;
             }
 #endif
+        }
+        if constexpr (PFX) {  // the prefix's path metric next to its rows; no decisions to output
+            const int64_t f = task * fpw + threadIdx.x;
+            if (f < B) *(double *)(P.pfx + (f << P.in_shift) + P.pm_off) = stv[0].pm;
+            wave_sync();  // the rows are reused by the next task, as after the tail below
+            continue;
         }
 #ifdef QPD_STAMPS
         __builtin_amdgcn_s_waitcnt(0);
@@ -1371,6 +1414,22 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
 #endif
     }
 }
+
+// ---------------------------------------------------------------------------
+// Frozen prefix (SCL-LUT in pre-mode): lut_fast_kernel<KIND, 1, false, false, true>.  Up to the first information leaf
+// every path of a frame holds the same rows -- path 0 is the only one with a
+// finite metric and all decisions are frozen zeros -- yet the decode kernel
+// would compute them L times (SCLLUTDecoder.cpp:62-104 before the first fork).
+// This kernel runs that op prefix once per frame, one lane per frame (gs = 1,
+// 64 frames per wave, the same op code and row layout), and leaves the rows
+// the rest of the schedule reads (OP_EXPORT) plus path 0's metric in the free
+// last quarter of the frame's pre-pass row.  The decode kernel then starts at
+// the first forking op: OP_IMPORT ops copy those rows into every path's own
+// column (and zero the prefix's partial-sum rows), and path 0 starts from the
+// prefix's metric.  The metric is accumulated by the same code in the same
+// leaf order, so the doubles are identical.
+// ---------------------------------------------------------------------------
+#define lut_prefix_kernel(KIND) lut_fast_kernel<KIND, 1, false, false, true>
 
 #ifndef QPD_FAST_TEMPLATES_ONLY  // qpd_fast_fscl.hip: the decode kernel templates only
 // ---------------------------------------------------------------------------

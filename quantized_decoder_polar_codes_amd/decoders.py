@@ -159,11 +159,12 @@ class _DecoderBase:
 
     def kernel_times(self) -> dict:
         """{class: (ms summed, launches)} since the last call, for the classes
-        'pre' (root pre-pass), 'decode' and 'mc' (frame generator)."""
+        'pre' (root pre-pass), 'decode', 'mc' (frame generator) and 'pfx'
+        (frozen prefix, lut_prefix_kernel)."""
         ms = (ctypes.c_double * _lib.QPD_KC_COUNT)()
         n = (ctypes.c_int64 * _lib.QPD_KC_COUNT)()
         _lib.check(_lib.load().qpd_kernel_times(self._h, ms, n))
-        return {name: (ms[i], n[i]) for i, name in enumerate(("pre", "decode", "mc"))}
+        return {name: (ms[i], n[i]) for i, name in enumerate(("pre", "decode", "mc", "pfx"))}
 
     # -- decoding --------------------------------------------------------------
     def decode_batch(self, x):

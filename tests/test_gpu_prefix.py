@@ -1,0 +1,114 @@
+"""Frozen-prefix split (lut_prefix_kernel, csrc/qpd_fast.hip): SCL-LUT (and
+CA-SCL-LUT) in pre-mode run the schedule up to the first information leaf once per frame and the
+decode kernel resumes from the exported rows and path metric.  The bits must
+equal the oracle's and the unsplit kernel's (QPD_NO_PFX=1) on every input:
+  * PW codes at the bench size (split present) and odd batch sizes;
+  * codes whose first bit is information (a prefix of f ops only) or whose
+    live rows do not fit the pre-pass row (the split is refused);
+  * CRC-aided kinds, whose tail checks every path's CRC.
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_frames_equal
+
+pytestmark = pytest.mark.gpu
+
+SPLIT = ("SCL-LUT",)  # the kinds that take the split (FastSCL's nodes already skip most of the prefix)
+
+
+@pytest.fixture(scope="module")
+def qpd(native_lib):
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    import quantized_decoder_polar_codes_amd as Q
+
+    return Q
+
+
+def _code(N, K):
+    from quantized_decoder_polar_codes_amd import codes as C
+
+    _, mb, fm, _ = C.construct_pw(N, K)
+    return fm, C.identify_nodes(N, mb).astype(np.int32)
+
+
+def _tables(N, seed):
+    from quantized_decoder_polar_codes_amd import lut as LU
+
+    return LU.random_luts(N, 16, seed=seed, distinct_mags=3)
+
+
+def _make(qpd, monkeypatch, kind, p, K, fm, L, nt, split, **kw):
+    if split:
+        monkeypatch.delenv("QPD_NO_PFX", raising=False)
+    else:
+        monkeypatch.setenv("QPD_NO_PFX", "1")
+    return qpd.from_packed(kind, p, K, fm, L=L, node_type=nt, **kw)
+
+
+@pytest.mark.parametrize("B", [24, 77])
+@pytest.mark.parametrize("kind", ["SCL-LUT", "FastSCL-LUT"])
+def test_prefix_matches_oracle(kind, B, qpd, oracle_mod, monkeypatch):
+    N, K, L = 1024, 512, 8
+    fm, nt = _code(N, K)
+    p = _tables(N, 7000 + B)
+    sym = np.random.default_rng(B).integers(0, 16, size=(B, N), dtype=np.int32)
+    dec = _make(qpd, monkeypatch, kind, p, K, fm, L, nt, True)
+    assert (dec.info()["prefix_ops"] > 0) == (kind in SPLIT)
+    want = oracle_mod.decode_lut(kind, p, K, L, fm, sym, node_type=nt)
+    assert_frames_equal(dec.decode_batch(sym), want, dec, f"prefix-{kind}-{B}")
+
+
+@pytest.mark.parametrize("N,K,L", [(1024, 512, 8), (1024, 256, 4), (512, 400, 8), (256, 64, 2), (128, 96, 16)])
+@pytest.mark.parametrize("kind", ["SCL-LUT", "FastSCL-LUT"])
+def test_prefix_equals_unsplit(kind, N, K, L, qpd, monkeypatch):
+    """Split and unsplit schedules give the same bits on noisy codewords and on
+    random symbols (4099 frames: a partial last task in both kernels)."""
+    import torch
+
+    from quantized_decoder_polar_codes_amd import lut as LU
+
+    fm, nt = _code(N, K)
+    if kind == "FastSCL-LUT" and 0 <= nt[0] <= 2:
+        pytest.skip("special root: undefined in the reference")
+    p = LU.minsum_uniform_luts(N)
+    rng = np.random.default_rng(N + K + L)
+    sym = rng.integers(0, 16, size=(4099, N), dtype=np.int32)
+    sym[: 2048] = np.clip(sym[: 2048] // 2 + 8, 0, 15)  # a biased half: long runs of confident symbols
+    a = _make(qpd, monkeypatch, kind, p, K, fm, L, nt, True)
+    b = _make(qpd, monkeypatch, kind, p, K, fm, L, nt, False)
+    assert b.info()["prefix_ops"] == 0
+    if L <= 8:
+        assert (a.info()["prefix_ops"] > 0) == (kind in SPLIT)
+    st = torch.from_numpy(sym).cuda()
+    ga, gb = a.decode_batch(st).cpu().numpy(), b.decode_batch(st).cpu().numpy()
+    assert np.array_equal(ga, gb), np.flatnonzero((ga != gb).any(1))[:10]
+
+
+@pytest.mark.parametrize("N,K", [(64, 64), (1024, 1024), (1024, 16)])
+def test_prefix_refused_or_exact(N, K, qpd, oracle_mod, monkeypatch):
+    """Every bit information (K = N: the prefix is only the f ops down to the
+    first leaf) or a long prefix (K = 16 of 1024: the live rows may reach past
+    the pre-pass row's free quarter and the split is refused): whatever the
+    plan chose, the bits are the oracle's."""
+    fm, nt = _code(N, K)
+    p = _tables(N, 31 + K)
+    sym = np.random.default_rng(K).integers(0, 16, size=(40, N), dtype=np.int32)
+    dec = _make(qpd, monkeypatch, "SCL-LUT", p, K, fm, 8, nt, True)
+    want = oracle_mod.decode_lut("SCL-LUT", p, K, 8, fm, sym, node_type=nt)
+    assert_frames_equal(dec.decode_batch(sym), want, dec, f"prefix-edge-{N}-{K}")
+
+
+@pytest.mark.parametrize("kind", ["CA-SCL-LUT", "CA-FastSCL-LUT"])
+def test_prefix_crc_aided(kind, qpd, monkeypatch):
+    N, A, K, L = 1024, 500, 512, 8
+    fm, nt = _code(N, K)
+    p = _tables(N, 99)
+    sym = np.random.default_rng(5).integers(0, 16, size=(24, N), dtype=np.int32)
+    a = _make(qpd, monkeypatch, kind, p, K, fm, L, nt, True, A=A)
+    b = _make(qpd, monkeypatch, kind, p, K, fm, L, nt, False, A=A)
+    assert (a.info()["prefix_ops"] > 0) == (kind[3:] in SPLIT)
+    ga = a.decode_batch(sym)
+    assert np.array_equal(ga, b.decode_batch(sym))

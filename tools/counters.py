@@ -37,9 +37,16 @@ agg = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(lambda: collections.defaultdict(set))
 short = {"lut_fast_kernel": "lut_fast_kernel", "root_pre_kernel": "root_pre_kernel",
          "generic_decode_kernel": "generic_decode_kernel", "mc_frames_kernel": "mc_frames_kernel"}
+def kernel_of(full):
+    # lut_fast_kernel<KIND, 1, false, false, true>: the frozen-prefix instantiation (PFX)
+    if "lut_fast_kernel" in full and "true>(" in full.replace(" ", ""):
+        return "lut_prefix_kernel"
+    return next((s for s in short if s in full), None)
+
+
 for p in paths:
     for r in csv.DictReader(open(p)):
-        name = next((s for s in short if s in r["Kernel_Name"]), None)
+        name = kernel_of(r["Kernel_Name"])
         if name is None:
             continue
         agg[name][r["Counter_Name"]] += float(r["Counter_Value"])

@@ -8,7 +8,8 @@ for path in sys.argv[2:]:
     agg = collections.defaultdict(float)
     nd = set()
     for r in csv.DictReader(open(path)):
-        if "lut_fast_kernel" in r["Kernel_Name"] or "lut_decode_kernel" in r["Kernel_Name"]:
+        kn = r["Kernel_Name"]
+        if ("lut_fast_kernel" in kn and "true>(" not in kn.replace(" ", "")) or "lut_decode_kernel" in kn:  # not the prefix
             agg[r["Counter_Name"]] += float(r["Counter_Value"])
             nd.add(r["Dispatch_Id"])
     print(f"# {path} ({len(nd)} dispatch(es))")
