@@ -310,8 +310,9 @@ def roofline(args, dec, kt, frames, calls):
     kc = (rec or {}).get("kernels", {}).get(kname, {})
     out = {"bound": "lds", "achieved": achieved, "peak": peak, "unit": "GB/s", "frac": achieved / peak,
            "traffic": kc.get("traffic"), "kernel": kname, "kernel_ms": dec_ms / max(1, n_dec), "launches": n_dec,
-           "prefix_kernel_ms": pfx_ms / max(1, n_pfx) if n_pfx else None,
-           "achieved_over": "lut_fast_kernel + lut_prefix_kernel per launch" if n_pfx else kname,
+           # frozen-prefix stages (lut_prefix_kernel): their summed time per decode launch
+           "prefix_kernel_ms": pfx_ms / max(1, n_dec) if n_pfx else None, "prefix_launches": n_pfx,
+           "achieved_over": "lut_fast_kernel + its lut_prefix_kernel stages per launch" if n_pfx else kname,
            "algorithmic_bytes_per_launch": onchip_per_frame * per_launch,
            "algorithmic": f"{onchip_per_frame} B/frame on-chip (SURVEY.md §8(d)) x {per_launch:.0f} frames per launch",
            "peak_probe": peaks, "lds_hit": kc.get("lds_hit"),

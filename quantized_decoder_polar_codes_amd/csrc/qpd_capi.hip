@@ -89,8 +89,12 @@ struct qpd_decoder {
     qpd::FastPlan fplan{};
     DeviceBuf f_tab, g_tab, fscratch, mops, r1_rank, task_ctr;
     int num_mops = 0;
-    DeviceBuf pfx_mops;  // frozen-prefix ops (lut_prefix_kernel); empty: no split
-    int pfx_nops = 0;
+    DeviceBuf pfx_mops;  // frozen-prefix stages' ops (lut_prefix_kernel): stage 1, then stage 2
+    int pfx_nops = 0;    // stage 1 (one path per frame); 0: no split
+    int pfx2_nops = 0;   // stage 2 (<= 4 live paths); 0: the decode kernel resumes from stage 1
+    int pfx2_rec = 0, pfx2_pm = 0;  // stage 2: words per path record, metric word in it
+    DeviceBuf pfx2_buf;  // stage 2's records: 4 paths x pfx2_rec words per frame
+    size_t pfx2_cap = 0;
     std::vector<Op> ops_host;
     DeviceBuf lut_f, f_base, lut_g, g_base, vcl, ops, info_pos, scratch, err;
     DeviceBuf r_f, r_g, q_bnd, q_rec, bnd_off, bnd_len, rec_off, rec_len;  // float-domain re-quantizers
@@ -507,15 +511,23 @@ void place_syncs(std::vector<qpd::MOp> &ops, bool list) {
     }
 }
 
-// Row ownership of a fast layout: (space, row) -> slot, for the prefix split.
+// Row ownership of a fast layout: (space, row) -> slot (0 R, 1 S, 2 U) and tree
+// depth, for the frozen-prefix split.
 struct FastOwner {
-    std::vector<int8_t> kind[2];  // per space (0 slab, 1 LDS): -1 unowned, 0 U/R row, 1 S row
-    void add(bool lds, int base, int cnt, bool srow) {
-        auto &k = kind[lds ? 1 : 0];
-        if ((int)k.size() < base + cnt) k.resize(base + cnt, -1);
-        for (int r = 0; r < cnt; ++r) k[base + r] = srow ? 1 : 0;
+    std::vector<int8_t> slot[2], depth[2];  // per space (0 slab, 1 LDS); slot -1: unowned
+    void add(bool lds, int base, int cnt, int sl, int dd) {
+        const int sp = lds ? 1 : 0;
+        if ((int)slot[sp].size() < base + cnt) {
+            slot[sp].resize(base + cnt, -1);
+            depth[sp].resize(base + cnt, -1);
+        }
+        for (int r = 0; r < cnt; ++r) {
+            slot[sp][base + r] = (int8_t)sl;
+            depth[sp][base + r] = (int8_t)dd;
+        }
     }
-    int of(int sp, int row) const { return row >= 0 && row < (int)kind[sp].size() ? kind[sp][row] : -1; }
+    int of(int sp, int row) const { return row >= 0 && row < (int)slot[sp].size() ? slot[sp][row] : -1; }
+    int rows(int sp) const { return (int)slot[sp].size(); }
 };
 
 // Rows of the fast engine's slab / LDS an op reads and writes (space, first
@@ -562,89 +574,158 @@ void op_rows(const qpd::MOp &m, Fn &&acc) {
     }
 }
 
-// Split a list decoder's schedule at its first forking op (see
-// lut_prefix_kernel): `pfx` = the ops before it + OP_EXPORT of every S row
-// word the rest reads before writing; `rest` = OP_IMPORT of those words (from
-// the pre-pass row) and zeros for the U / R words (every prefix decision is a
-// frozen 0) + the ops from the fork on.  False (no split) when there is no
-// prefix, the live rows are not S / U / R rows, or they do not fit the free
-// quarter of the pre-pass row next to the metric.
-bool split_prefix(const std::vector<qpd::MOp> &ops, const FastOwner &own, int N, std::vector<qpd::MOp> &pfx,
-                  std::vector<qpd::MOp> &rest) {
+// Frozen-prefix stages of an SCL schedule (see lut_prefix_kernel).
+//   stage 1: ops [0, s1) -- up to the first forking op: one path, gs = 1;
+//   stage 2: ops [s1, s2) -- up to the op with the third information leaf: at
+//            most 4 live paths, run with L = 4 (the stable selection keeps the
+//            live paths in slots 0-3 in the same order as with L = 8, and the
+//            other slots' metrics are infinite);
+//   decode:  ops [s2, end) with the full list.
+// Each stage ends with OP_EXPORT of the words the later ops read before
+// writing them (live-in) and begins with OP_IMPORT of its predecessor's.
+struct PrefixPlan {
+    std::vector<qpd::MOp> st1, st2, rest;
+    int rec2 = 0, pm2 = 0;  // stage 2: words per path record, metric word in it
+};
+
+bool is_fork(const qpd::MOp &m) {
     using namespace qpd;
-    size_t s = 0;
-    for (; s < ops.size(); ++s) {
-        const MOp &m = ops[s];
-        const bool forks = (m.type == OP_BOT3 && m.cnt != 0xff) || ((m.type == OP_LEAF_L || m.type == OP_LEAF_R) && m.cnt == 0) ||
-                           m.type == OP_R1 || m.type == OP_REP || m.type == OP_SPC;
-        if (forks) break;
-    }
-    if (s == 0 || s == ops.size()) return false;
-    // live-in words of the rest: read before any op of the rest writes them
-    std::vector<char> def[2], live[2];
+    return (m.type == OP_BOT3 && m.cnt != 0xff) || ((m.type == OP_LEAF_L || m.type == OP_LEAF_R) && m.cnt == 0) ||
+           m.type == OP_R1 || m.type == OP_REP || m.type == OP_SPC;
+}
+
+int info_leaves(const qpd::MOp &m) {
+    using namespace qpd;
+    if (m.type == OP_BOT3) return __builtin_popcount(~m.cnt & 0xff);
+    if (m.type == OP_LEAF_L || m.type == OP_LEAF_R) return m.cnt == 0;
+    return 0;
+}
+
+// Live-in words of ops[from, end): live[sp][row].  False if an unowned row is read.
+bool live_in(const std::vector<qpd::MOp> &ops, size_t from, const FastOwner &own, std::vector<char> (&live)[2]) {
+    std::vector<char> def[2];
     for (int sp = 0; sp < 2; ++sp) {
-        def[sp].assign(own.kind[sp].size() + 1, 0);
-        live[sp].assign(own.kind[sp].size() + 1, 0);
+        def[sp].assign(own.rows(sp), 0);
+        live[sp].assign(own.rows(sp), 0);
     }
     bool ok = true;
-    for (size_t i = s; i < ops.size() && ok; ++i) {
+    for (size_t i = from; i < ops.size() && ok; ++i)
         op_rows(ops[i], [&](bool wr, int sp, int row, int cnt) {
             for (int r = row; r < row + cnt; ++r) {
                 if (own.of(sp, r) < 0) {
-                    if (!wr) ok = false;  // an unowned row read (scratch): no split
+                    if (!wr) ok = false;
                     continue;
                 }
                 if (wr) def[sp][r] = 1;
                 else if (!def[sp][r]) live[sp][r] = 1;
             }
         });
-    }
-    if (!ok) return false;
-    const int q0 = 3 * (N / 16), pm_off = N / 4 - 2;  // free quarter: [q0, pm_off) rows, then the metric
-    int at = q0;
-    std::vector<MOp> imp, exp;
+    return ok;
+}
+
+// Runs of live words with one slot and depth: fn(sp, first row, count, slot, depth).
+template <class Fn>
+void live_runs(const std::vector<char> (&live)[2], const FastOwner &own, Fn &&fn) {
     for (int sp = 0; sp < 2; ++sp)
-        for (int r = 0; r < (int)own.kind[sp].size();) {
+        for (int r = 0; r < own.rows(sp);) {
             if (!live[sp][r]) {
                 ++r;
                 continue;
             }
-            const int k = own.of(sp, r);
             int e = r;
-            while (e < (int)own.kind[sp].size() && live[sp][e] && own.of(sp, e) == k) ++e;
-            MOp m;
-            std::memset(&m, 0, sizeof(m));
-            m.type = OP_IMPORT;
-            m.dst_row = r;
-            m.cnt = e - r;
-            m.flags = sp ? MF_DST_LDS : 0;
-            if (k == 1) {  // S row words: computed by the prefix
-                if (at + m.cnt > pm_off) return false;
-                m.flags |= MF_PRE;
-                m.src_row = at;
-                MOp x = m;
-                x.type = OP_EXPORT;
-                x.flags = sp ? MF_SRC_LDS : 0;
-                x.src_row = r;
-                x.dst_row = at;
-                exp.push_back(x);
-                at += m.cnt;
-            } else {
-                m.flags |= MF_ZERO;
-            }
-            imp.push_back(m);
+            while (e < own.rows(sp) && live[sp][e] && own.slot[sp][e] == own.slot[sp][r] && own.depth[sp][e] == own.depth[sp][r])
+                ++e;
+            fn(sp, r, e - r, (int)own.slot[sp][r], (int)own.depth[sp][r]);
             r = e;
         }
-    MOp pm;  // path 0's metric
-    std::memset(&pm, 0, sizeof(pm));
-    pm.type = OP_IMPORT;
+}
+
+qpd::MOp blank_op(int type) {
+    qpd::MOp m;
+    std::memset(&m, 0, sizeof(m));
+    m.type = type;
+    return m;
+}
+
+bool plan_prefix(const std::vector<qpd::MOp> &ops, const FastOwner &own, int N, int L, PrefixPlan &pp) {
+    using namespace qpd;
+    size_t s1 = 0;
+    while (s1 < ops.size() && !is_fork(ops[s1])) ++s1;
+    if (s1 == 0 || s1 == ops.size()) return false;
+    // stage 1 -> pre-pass row quarter [3N/16, N/4 - 2) + the metric at N/4 - 2: S words
+    // (computed), U / R words are zeros (every decision of the prefix is a frozen 0)
+    std::vector<char> live1[2];
+    if (!live_in(ops, s1, own, live1)) return false;
+    const int pm1 = N / 4 - 2;
+    int at = 3 * (N / 16);
+    std::vector<MOp> imp1, exp1;
+    bool fits = true;
+    live_runs(live1, own, [&](int sp, int r, int cnt, int slot, int) {
+        MOp m = blank_op(OP_IMPORT);
+        m.dst_row = r;
+        m.cnt = cnt;
+        m.flags = sp ? MF_DST_LDS : 0;
+        if (slot == 1) {
+            if (at + cnt > pm1) fits = false;
+            m.flags |= MF_PRE;
+            m.src_row = at;
+            MOp x = blank_op(OP_EXPORT);
+            x.flags = sp ? MF_SRC_LDS : 0;
+            x.src_row = r;
+            x.dst_row = at;
+            x.cnt = cnt;
+            exp1.push_back(x);
+            at += cnt;
+        } else {
+            m.flags |= MF_ZERO;
+        }
+        imp1.push_back(m);
+    });
+    if (!fits) return false;
+    MOp pm = blank_op(OP_IMPORT);
     pm.flags = MF_PRE | MF_PM;
-    pm.src_row = pm_off;
-    imp.insert(imp.begin(), pm);
-    pfx.assign(ops.begin(), ops.begin() + s);
-    pfx.insert(pfx.end(), exp.begin(), exp.end());
-    rest = imp;
-    rest.insert(rest.end(), ops.begin() + s, ops.end());
+    pm.src_row = pm1;
+    imp1.insert(imp1.begin(), pm);
+    pp.st1.assign(ops.begin(), ops.begin() + s1);
+    pp.st1.insert(pp.st1.end(), exp1.begin(), exp1.end());
+    // stage 2 (L > 4): up to the op with the third information leaf
+    size_t s2 = s1;
+    for (int inf = 0; s2 < ops.size() && inf + info_leaves(ops[s2]) <= 2; ++s2) inf += info_leaves(ops[s2]);
+    std::vector<char> live2[2];
+    if (L <= 4 || getenv("QPD_NO_PFX2") || s2 <= s1 || s2 >= ops.size() || !live_in(ops, s2, own, live2)) {
+        pp.rest = imp1;
+        pp.rest.insert(pp.rest.end(), ops.begin() + s1, ops.end());
+        return true;
+    }
+    std::vector<MOp> imp2, exp2;
+    int w2 = 0;
+    live_runs(live2, own, [&](int sp, int r, int cnt, int slot, int dd) {
+        MOp x = blank_op(OP_EXPORT);  // read through the lineage's pointer of that depth
+        x.flags = (sp ? MF_SRC_LDS : 0) | (slot == 1 ? MF_VIA_PS : slot == 2 ? MF_VIA_PU : 0);
+        x.sh_src = 4 * dd;
+        x.src_row = r;
+        x.dst_row = w2;
+        x.cnt = cnt;
+        exp2.push_back(x);
+        MOp m = blank_op(OP_IMPORT);
+        m.flags = MF_XBUF | (sp ? MF_DST_LDS : 0);
+        m.src_row = w2;
+        m.dst_row = r;
+        m.cnt = cnt;
+        imp2.push_back(m);
+        w2 += cnt;
+    });
+    pp.pm2 = (w2 + 1) & ~1;
+    pp.rec2 = pp.pm2 + 2;
+    MOp pm2 = blank_op(OP_IMPORT);
+    pm2.flags = MF_XBUF | MF_PM;
+    pm2.src_row = pp.pm2;
+    imp2.insert(imp2.begin(), pm2);
+    pp.st2 = imp1;
+    pp.st2.insert(pp.st2.end(), ops.begin() + s1, ops.begin() + s2);
+    pp.st2.insert(pp.st2.end(), exp2.begin(), exp2.end());
+    pp.rest = imp2;
+    pp.rest.insert(pp.rest.end(), ops.begin() + s2, ops.end());
     return true;
 }
 
@@ -838,37 +919,39 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
         if (rc) return rc;
     }
     F.r1_rank = (const uint16_t *)d->r1_rank.p;
-    // Frozen-prefix split (lut_prefix_kernel): list kinds in pre-mode.
-    std::vector<qpd::MOp> pfx;
+    // Frozen-prefix stages (lut_prefix_kernel, plan_prefix): SCL-LUT in pre-mode.
+    // FastSCL's R0 / REP nodes already take most of the prefix (4 ops of the bench
+    // code; the one-stage split measured -3 % there, profiles/r03ab_*).
+    PrefixPlan pp;
     F.pm_off = -1;
-    // SCL-LUT only: FastSCL's R0 / REP nodes already take most of the prefix (4 ops of the
-    // bench code; the split measured -3 %, profiles/r03ab_*)
+    F.xin_paths = 1;
     if (Ly.pre && d->L > 1 && c->kind == QPD_SCL_LUT && !getenv("QPD_NO_PFX")) {
         FastOwner own;
         for (int dd = 0; dd <= n; ++dd)
             for (int sl = 0; sl < 3; ++sl) {
                 const int b = sl == 0 ? Ly.R[dd] : sl == 1 ? Ly.S[dd] : Ly.U[dd];
-                const int cnt = use[sl][dd] ? rows_of(sl, dd) : 0;
-                own.add(Ly.lds(dd), b, cnt, sl == 1);
+                own.add(Ly.lds(dd), b, use[sl][dd] ? rows_of(sl, dd) : 0, sl == 0 ? 0 : sl == 1 ? 1 : 2, dd);
             }
-        std::vector<qpd::MOp> rest;
-        if (split_prefix(mops, own, N, pfx, rest)) {
-            mops.swap(rest);
-            F.pm_off = N / 4 - 2;  // the prefix kernel's metric word (split_prefix)
-        }
+        if (plan_prefix(mops, own, N, d->L, pp)) mops.swap(pp.rest);
     }
-    place_syncs(pfx, true);
+    place_syncs(pp.st1, true);
+    place_syncs(pp.st2, true);
     place_syncs(mops, c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT);
-    d->pfx_nops = (int)pfx.size();
-    if (!pfx.empty()) {
-        int rc = upload(d->pfx_mops, pfx.data(), pfx.size(), d->hs);
+    d->pfx_nops = (int)pp.st1.size();
+    d->pfx2_nops = (int)pp.st2.size();
+    d->pfx2_rec = pp.rec2;
+    d->pfx2_pm = pp.pm2;
+    std::vector<qpd::MOp> allp = pp.st1;  // one device array: stage 1, then stage 2
+    allp.insert(allp.end(), pp.st2.begin(), pp.st2.end());
+    if (!allp.empty()) {
+        int rc = upload(d->pfx_mops, allp.data(), allp.size(), d->hs);
         if (rc) return rc;
     }
     for (const qpd::MOp &m : mops)  // R1 nodes the register/LDS argsort cannot take
         if (c->kind == QPD_FASTSCL_LUT && m.type == qpd::OP_R1 && m.cnt > qpd::stl::kThreshold && !(m.flags & qpd::MF_R1_LDS))
             d->r1l = true;
     F.nops = (int)mops.size();
-    d->num_mops = F.nops + d->pfx_nops;
+    d->num_mops = F.nops + d->pfx_nops + d->pfx2_nops;
     {
         int rc = upload(d->mops, mops.data(), mops.size(), d->hs);
         if (rc) return rc;
@@ -1260,7 +1343,7 @@ int qpd_get_info(const qpd_decoder *d, qpd_info *info) {
     info->engine = d->engine;
     info->lds_bytes_per_wave = d->lds_bytes;
     info->lds_from_depth = d->engine == QPD_ENGINE_FAST ? d->fplan.lds_from : -1;
-    info->prefix_ops = d->engine == QPD_ENGINE_FAST ? d->pfx_nops : 0;
+    info->prefix_ops = d->engine == QPD_ENGINE_FAST ? d->pfx_nops + d->pfx2_nops : 0;
     return QPD_OK;
 }
 
@@ -1303,7 +1386,7 @@ int decode_pre_rows(qpd_decoder *d, const uint32_t *rows, int64_t Bc, uint8_t *o
     qpd::FastPlan fp = d->fplan;
     fp.in_vec = 1;
     fp.in_shift = fp.n - 2;
-    if (d->pfx_nops > 0) {  // the frozen prefix once per frame, into the rows' free quarter
+    if (d->pfx_nops > 0) {  // stage 1: the frozen prefix once per frame, into the rows' free quarter
         qpd::FastPlan pp = fp;
         pp.ops = (const qpd::MOp *)d->pfx_mops.p;
         pp.nops = d->pfx_nops;
@@ -1311,8 +1394,38 @@ int decode_pre_rows(qpd_decoder *d, const uint32_t *rows, int64_t Bc, uint8_t *o
         pp.fpw = 64;
         pp.L = 1;
         pp.pfx = const_cast<uint32_t *>(rows);
+        pp.pfx_fstride = fp.N / 4;
+        pp.pfx_pstride = 0;
+        pp.pm_off = fp.N / 4 - 2;
         const int rc = fast_launch(d, pp, (const int32_t *)rows, Bc, nullptr, st, true);
         if (rc) return rc;
+    }
+    if (d->pfx2_nops > 0) {  // stage 2: <= 4 live paths, L = 4, into per-path records
+        const size_t need = (size_t)Bc * 4 * d->pfx2_rec * sizeof(uint32_t);
+        if (d->pfx2_cap < need) {
+            if (d->pfx2_buf.p) (void)hipFree(d->pfx2_buf.p);
+            d->pfx2_buf.p = nullptr;
+            d->pfx2_cap = 0;
+            const hipError_t e = hipMalloc(&d->pfx2_buf.p, need);
+            if (e != hipSuccess) return fail(QPD_E_DEVICE, std::string("prefix records hipMalloc: ") + hipGetErrorString(e));
+            d->pfx2_cap = need;
+        }
+        qpd::FastPlan pp = fp;
+        pp.ops = (const qpd::MOp *)d->pfx_mops.p + d->pfx_nops;
+        pp.nops = d->pfx2_nops;
+        pp.gs = 4;
+        pp.fpw = 16;
+        pp.L = 4;
+        pp.pfx = (uint32_t *)d->pfx2_buf.p;
+        pp.pfx_fstride = 4 * d->pfx2_rec;
+        pp.pfx_pstride = d->pfx2_rec;
+        pp.pm_off = d->pfx2_pm;
+        const int rc = fast_launch(d, pp, (const int32_t *)rows, Bc, nullptr, st, true);
+        if (rc) return rc;
+        fp.xin = (const uint32_t *)d->pfx2_buf.p;
+        fp.xin_fstride = 4 * d->pfx2_rec;
+        fp.xin_pstride = d->pfx2_rec;
+        fp.xin_paths = 4;
     }
     return fast_launch(d, fp, (const int32_t *)rows, Bc, out, st);
 }

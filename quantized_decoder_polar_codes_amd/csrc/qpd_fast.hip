@@ -52,7 +52,10 @@ enum MopFlag : int32_t {
     MF_VUNI = 8192,   // special node whose elements share one quanta row (v <= 16): quanta and
                       //   R1 ranks are looked up in a register row instead of gathered per element
     MF_ZERO = 16384,  // OP_IMPORT: zero rows (partial sums of the frozen prefix) instead of pre-row words
-    MF_PM = 32768,    // OP_IMPORT: path 0's metric (a double at word src_row of the pre-pass row)
+    MF_PM = 32768,    // OP_IMPORT: the path metric (a double at word src_row of the source record)
+    MF_VIA_PS = 65536,   // OP_EXPORT: the row is read through the path's S pointer of depth sh_src / 4
+    MF_VIA_PU = 131072,  //   ... or its U pointer (else the lane's own row: R rows)
+    MF_XBUF = 262144,    // OP_IMPORT: from the previous prefix stage's per-path records (P.xin), not the pre-pass row
 };
 
 struct MOp {
@@ -93,10 +96,18 @@ struct FastPlan {
     int32_t *err;
     uint32_t *task_ctr;           // QPD_DYN task queue: tasks taken (never reset; see wave_take)
     uint32_t task_base;           // per launch: the counter's value when this launch's takes begin
-    // lut_prefix_kernel: the pre-pass rows, writable (the prefix's live rows and path
-    // metric go to the free last quarter of each frame's row; the metric at pm_off)
+    // Frozen-prefix stages (lut_prefix_kernel).  A stage writes, per frame f and path
+    // gl, its live rows (OP_EXPORT) and metric (word pm_off) to the record at
+    // pfx + f * pfx_fstride + gl * pfx_pstride: stage 1 (one path) into the free last
+    // quarter of the pre-pass row, stage 2 (live paths <= 4) into a buffer of its own.
+    // OP_IMPORT with MF_XBUF reads such records back (xin: xin_paths live paths; the
+    // other paths of the frame start from path 0's rows with an infinite metric).
     uint32_t *pfx;
-    int32_t pm_off;
+    int64_t pfx_fstride;
+    int32_t pfx_pstride, pm_off;
+    const uint32_t *xin;
+    int64_t xin_fstride;
+    int32_t xin_pstride, xin_paths;
 };
 
 // Timing experiments only (wrong results): 0 = every op reads node 0's
@@ -1238,26 +1249,36 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
                     break;
                 }
                 case OP_IMPORT:
-                    if constexpr (KIND == K_SCL_LUT && !PFX) {  // the frozen prefix's results (lut_prefix_kernel)
-                        if (fl & MF_PM) {  // path 0 resumes from the prefix's metric
+                    if constexpr (KIND == K_SCL_LUT) {  // a frozen-prefix stage's results (lut_prefix_kernel)
+                        const bool xb = fl & MF_XBUF;
+                        const int live = xb ? P.xin_paths : 1;
 #pragma unroll
-                            for (int s = 0; s < NS; ++s)
-                                stv[s].pm = gl == 0 ? *(const double *)(yv[s] + op.src_row) : kInf;
-                        } else {  // its live rows, into every path's own column
-                            const bool dl = fl & MF_DST_LDS, z = fl & MF_ZERO;
-#pragma unroll
-                            for (int s = 0; s < NS; ++s)
-                                for (int w = 0; w < op.cnt; ++w)
-                                    Mv[s].st(dl, op.dst_row + w, lane, z ? 0u : ((const uint32_t *)yv[s])[op.src_row + w]);
+                        for (int s = 0; s < NS; ++s) {
+                            const uint32_t *src = (const uint32_t *)yv[s];
+                            if (xb) {  // the record of this lane's path (dead paths: path 0's)
+                                int64_t f = (task * NS + s) * fpw + (lane >> gsh);
+                                if (f >= B) f = B - 1;
+                                src = P.xin + f * P.xin_fstride + (gl < live ? gl : 0) * P.xin_pstride;
+                            }
+                            if (fl & MF_PM) {
+                                stv[s].pm = gl < live ? *(const double *)(src + op.src_row) : kInf;
+                            } else {  // live rows into every path's own column
+                                const bool dl = fl & MF_DST_LDS, z = fl & MF_ZERO;
+                                for (int w = 0; w < op.cnt; ++w) Mv[s].st(dl, op.dst_row + w, lane, z ? 0u : src[op.src_row + w]);
+                            }
                         }
                     }
                     break;
                 case OP_EXPORT:
-                    if constexpr (KIND == K_SCL_LUT && PFX) {  // one frame per lane (gs = 1, one set)
-                        const int64_t f = task * fpw + lane;
+                    if constexpr (KIND == K_SCL_LUT && PFX) {  // one set; the row of this path's lineage
+                        const int64_t f = task * fpw + (lane >> gsh);
+                        const int at = (fl & MF_VIA_PS)   ? gbase + pfield(stv[0].ps, op.sh_src)
+                                       : (fl & MF_VIA_PU) ? gbase + pfield(stv[0].pu, op.sh_src)
+                                                          : lane;
+                        uint32_t *dst = P.pfx + f * P.pfx_fstride + gl * P.pfx_pstride + op.dst_row;
                         for (int w = 0; w < op.cnt; ++w) {
-                            const uint32_t x = Mv[0].ld(fl & MF_SRC_LDS, op.src_row + w, lane);
-                            if (f < B) P.pfx[(f << P.in_shift) + op.dst_row + w] = x;
+                            const uint32_t x = Mv[0].ld(fl & MF_SRC_LDS, op.src_row + w, at);
+                            if (f < B) dst[w] = x;
                         }
                     }
                     break;
@@ -1288,9 +1309,10 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
             }
 #endif
         }
-        if constexpr (PFX) {  // the prefix's path metric next to its rows; no decisions to output
-            const int64_t f = task * fpw + threadIdx.x;
-            if (f < B) *(double *)(P.pfx + (f << P.in_shift) + P.pm_off) = stv[0].pm;
+        if constexpr (PFX) {  // the stage's path metrics next to its rows; no decisions to output
+            const int64_t f = task * fpw + (threadIdx.x >> __builtin_ctz(gs));
+            const int gl = threadIdx.x & (gs - 1);
+            if (f < B) *(double *)(P.pfx + f * P.pfx_fstride + gl * P.pfx_pstride + P.pm_off) = stv[0].pm;
             wave_sync();  // the rows are reused by the next task, as after the tail below
             continue;
         }
