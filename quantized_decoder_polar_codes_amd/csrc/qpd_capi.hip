@@ -95,6 +95,8 @@ struct qpd_decoder {
     int pfx2_rec = 0, pfx2_pm = 0;  // stage 2: words per path record, metric word in it
     DeviceBuf pfx2_buf;  // stage 2's records: 4 paths x pfx2_rec words per frame
     size_t pfx2_cap = 0;
+    std::vector<qpd::MOp> xin_ops;  // the decode ops' stage-2 imports, patched with pfx2_buf's address
+    const void *xin_at = nullptr;   // the address the device copies hold
     std::vector<Op> ops_host;
     DeviceBuf lut_f, f_base, lut_g, g_base, vcl, ops, info_pos, scratch, err;
     DeviceBuf r_f, r_g, q_bnd, q_rec, bnd_off, bnd_len, rec_off, rec_len;  // float-domain re-quantizers
@@ -586,6 +588,7 @@ void op_rows(const qpd::MOp &m, Fn &&acc) {
 struct PrefixPlan {
     std::vector<qpd::MOp> st1, st2, rest;
     int rec2 = 0, pm2 = 0;  // stage 2: words per path record, metric word in it
+    int nimp2 = 0;          // the decode ops' first nimp2 ops: stage-2 imports (MF_XBUF)
 };
 
 bool is_fork(const qpd::MOp &m) {
@@ -721,6 +724,12 @@ bool plan_prefix(const std::vector<qpd::MOp> &ops, const FastOwner &own, int N, 
     pm2.flags = MF_XBUF | MF_PM;
     pm2.src_row = pp.pm2;
     imp2.insert(imp2.begin(), pm2);
+    for (MOp &m : imp2) {  // record strides (words) and live paths; the address is patched per buffer
+        m.tab = 4 * pp.rec2;
+        m.vrow = pp.rec2;
+        m.tab2 = 4;
+    }
+    pp.nimp2 = (int)imp2.size();
     pp.st2 = imp1;
     pp.st2.insert(pp.st2.end(), ops.begin() + s1, ops.begin() + s2);
     pp.st2.insert(pp.st2.end(), exp2.begin(), exp2.end());
@@ -924,7 +933,6 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     // code; the one-stage split measured -3 % there, profiles/r03ab_*).
     PrefixPlan pp;
     F.pm_off = -1;
-    F.xin_paths = 1;
     if (Ly.pre && d->L > 1 && c->kind == QPD_SCL_LUT && !getenv("QPD_NO_PFX")) {
         FastOwner own;
         for (int dd = 0; dd <= n; ++dd)
@@ -941,6 +949,7 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     d->pfx2_nops = (int)pp.st2.size();
     d->pfx2_rec = pp.rec2;
     d->pfx2_pm = pp.pm2;
+    d->xin_ops.assign(mops.begin(), mops.begin() + (d->pfx2_nops > 0 ? pp.nimp2 : 0));
     std::vector<qpd::MOp> allp = pp.st1;  // one device array: stage 1, then stage 2
     allp.insert(allp.end(), pp.st2.begin(), pp.st2.end());
     if (!allp.empty()) {
@@ -1420,12 +1429,18 @@ int decode_pre_rows(qpd_decoder *d, const uint32_t *rows, int64_t Bc, uint8_t *o
         pp.pfx_fstride = 4 * d->pfx2_rec;
         pp.pfx_pstride = d->pfx2_rec;
         pp.pm_off = d->pfx2_pm;
+        if (d->xin_at != d->pfx2_buf.p) {  // the decode's import ops carry the records' address
+            const uint64_t a = (uint64_t)(uintptr_t)d->pfx2_buf.p;
+            for (qpd::MOp &m : d->xin_ops) {
+                m.u_row = (int32_t)(uint32_t)a;
+                m.r_row = (int32_t)(uint32_t)(a >> 32);
+            }
+            QPD_HIP(hipMemcpyAsync(d->mops.p, d->xin_ops.data(), d->xin_ops.size() * sizeof(qpd::MOp),
+                                   hipMemcpyHostToDevice, st));
+            d->xin_at = d->pfx2_buf.p;
+        }
         const int rc = fast_launch(d, pp, (const int32_t *)rows, Bc, nullptr, st, true);
         if (rc) return rc;
-        fp.xin = (const uint32_t *)d->pfx2_buf.p;
-        fp.xin_fstride = 4 * d->pfx2_rec;
-        fp.xin_pstride = d->pfx2_rec;
-        fp.xin_paths = 4;
     }
     return fast_launch(d, fp, (const int32_t *)rows, Bc, out, st);
 }

@@ -55,7 +55,7 @@ enum MopFlag : int32_t {
     MF_PM = 32768,    // OP_IMPORT: the path metric (a double at word src_row of the source record)
     MF_VIA_PS = 65536,   // OP_EXPORT: the row is read through the path's S pointer of depth sh_src / 4
     MF_VIA_PU = 131072,  //   ... or its U pointer (else the lane's own row: R rows)
-    MF_XBUF = 262144,    // OP_IMPORT: from the previous prefix stage's per-path records (P.xin), not the pre-pass row
+    MF_XBUF = 262144,    // OP_IMPORT: from the stage-2 per-path records (address in the op record), not the pre-pass row
 };
 
 struct MOp {
@@ -100,14 +100,12 @@ struct FastPlan {
     // gl, its live rows (OP_EXPORT) and metric (word pm_off) to the record at
     // pfx + f * pfx_fstride + gl * pfx_pstride: stage 1 (one path) into the free last
     // quarter of the pre-pass row, stage 2 (live paths <= 4) into a buffer of its own.
-    // OP_IMPORT with MF_XBUF reads such records back (xin: xin_paths live paths; the
-    // other paths of the frame start from path 0's rows with an infinite metric).
+    // OP_IMPORT with MF_XBUF reads stage-2 records back; the buffer address and strides
+    // ride in the op record (u_row | r_row << 32, tab, vrow, tab2 live paths), not in
+    // the plan: plan fields the decode loop reads cost it SGPRs (spill 149 -> 158).
     uint32_t *pfx;
     int64_t pfx_fstride;
     int32_t pfx_pstride, pm_off;
-    const uint32_t *xin;
-    int64_t xin_fstride;
-    int32_t xin_pstride, xin_paths;
 };
 
 // Timing experiments only (wrong results): 0 = every op reads node 0's
@@ -1251,14 +1249,15 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
                 case OP_IMPORT:
                     if constexpr (KIND == K_SCL_LUT) {  // a frozen-prefix stage's results (lut_prefix_kernel)
                         const bool xb = fl & MF_XBUF;
-                        const int live = xb ? P.xin_paths : 1;
+                        const int live = xb ? op.tab2 : 1;
 #pragma unroll
                         for (int s = 0; s < NS; ++s) {
                             const uint32_t *src = (const uint32_t *)yv[s];
                             if (xb) {  // the record of this lane's path (dead paths: path 0's)
                                 int64_t f = (task * NS + s) * fpw + (lane >> gsh);
                                 if (f >= B) f = B - 1;
-                                src = P.xin + f * P.xin_fstride + (gl < live ? gl : 0) * P.xin_pstride;
+                                const uint32_t *base = (const uint32_t *)(((uint64_t)(uint32_t)op.r_row << 32) | (uint32_t)op.u_row);
+                                src = base + f * op.tab + (gl < live ? gl : 0) * op.vrow;
                             }
                             if (fl & MF_PM) {
                                 stv[s].pm = gl < live ? *(const double *)(src + op.src_row) : kInf;
