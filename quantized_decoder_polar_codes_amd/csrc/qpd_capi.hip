@@ -92,6 +92,7 @@ struct qpd_decoder {
     DeviceBuf pfx_mops;  // frozen-prefix stages' ops (lut_prefix_kernel): stage 1, then stage 2
     int pfx_nops = 0;    // stage 1 (one path per frame); 0: no split
     int pfx2_nops = 0;   // stage 2 (<= 4 live paths); 0: the decode kernel resumes from stage 1
+    int pfx_sets = 1;    // frame sets per wave of the prefix stages (QPD_PFX_SETS)
     int pfx2_rec = 0, pfx2_pm = 0;  // stage 2: words per path record, metric word in it
     DeviceBuf pfx2_buf;  // stage 2's records: 4 paths x pfx2_rec words per frame
     size_t pfx2_cap = 0;
@@ -774,10 +775,12 @@ const void *fast_kernel(int kind, int sets, bool l8, bool r1l) {
 #undef QPD_FK
 }
 
-const void *prefix_kernel(int kind) {
+const void *prefix_kernel(int kind, int sets) {
     using namespace qpd;
     switch (kind) {
-        case QPD_SCL_LUT: return reinterpret_cast<const void *>(&lut_prefix_kernel(K_SCL_LUT));
+        case QPD_SCL_LUT:
+            return sets == 2 ? reinterpret_cast<const void *>(&lut_prefix_kernel(K_SCL_LUT, 2))
+                             : reinterpret_cast<const void *>(&lut_prefix_kernel(K_SCL_LUT, 1));
         default: return nullptr;
     }
 }
@@ -946,6 +949,8 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     place_syncs(pp.st2, true);
     place_syncs(mops, c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT);
     d->pfx_nops = (int)pp.st1.size();
+    d->pfx_sets = std::min(d->sets, 2);
+    if (const char *e = getenv("QPD_PFX_SETS")) d->pfx_sets = std::min(d->sets, std::max(1, atoi(e)));
     d->pfx2_nops = (int)pp.st2.size();
     d->pfx2_rec = pp.rec2;
     d->pfx2_pm = pp.pm2;
@@ -1366,8 +1371,9 @@ namespace {
 // (channel symbols, in_shift = n; or pre-pass rows, in_shift = n - 2).
 int fast_launch(qpd_decoder *d, qpd::FastPlan fp, const int32_t *in, int64_t Bc, uint8_t *out, hipStream_t st,
                 bool prefix = false) {
-    const int64_t tw = (int64_t)fp.fpw * (prefix ? 1 : d->sets);  // frames per wave task
-    const void *kfn = prefix ? prefix_kernel(d->kind) : fast_kernel(d->kind, d->sets, d->l8, d->r1l);
+    const int sets = prefix ? d->pfx_sets : d->sets;
+    const int64_t tw = (int64_t)fp.fpw * sets;  // frames per wave task
+    const void *kfn = prefix ? prefix_kernel(d->kind, sets) : fast_kernel(d->kind, d->sets, d->l8, d->r1l);
     if (!kfn) return fail(QPD_E_INVALID, "bad kind");
     const int64_t fgroups = (Bc + tw - 1) / tw;
     int fgrid = (int)std::min<int64_t>(fgroups, d->max_waves);
@@ -1379,8 +1385,8 @@ int fast_launch(qpd_decoder *d, qpd::FastPlan fp, const int32_t *in, int64_t Bc,
     const qpd::MOp *ops_arg = fp.ops;
     fp.task_base = d->task_base;
     void *args[] = {&fp, &in, &Bc, &out, &ops_arg};
-    // the prefix kernel runs one frame set per wave in the same per-set layout
-    const size_t lds = (size_t)(prefix ? d->lds_bytes / d->sets : d->lds_bytes);
+    // the prefix stages run pfx_sets frame sets per wave in the same per-set layout
+    const size_t lds = (size_t)(d->lds_bytes / d->sets * sets);
     const int rc = timed_launch(d, prefix ? QPD_KC_PFX : QPD_KC_DECODE, st, [&]() -> int {
         QPD_HIP(hipLaunchKernel(kfn, dim3(fgrid), dim3(64), args, lds, st));
         QPD_HIP(hipGetLastError());

@@ -1269,15 +1269,18 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
                     }
                     break;
                 case OP_EXPORT:
-                    if constexpr (KIND == K_SCL_LUT && PFX) {  // one set; the row of this path's lineage
-                        const int64_t f = task * fpw + (lane >> gsh);
-                        const int at = (fl & MF_VIA_PS)   ? gbase + pfield(stv[0].ps, op.sh_src)
-                                       : (fl & MF_VIA_PU) ? gbase + pfield(stv[0].pu, op.sh_src)
-                                                          : lane;
-                        uint32_t *dst = P.pfx + f * P.pfx_fstride + gl * P.pfx_pstride + op.dst_row;
-                        for (int w = 0; w < op.cnt; ++w) {
-                            const uint32_t x = Mv[0].ld(fl & MF_SRC_LDS, op.src_row + w, at);
-                            if (f < B) dst[w] = x;
+                    if constexpr (KIND == K_SCL_LUT && PFX) {  // the row of this path's lineage
+#pragma unroll
+                        for (int s = 0; s < NS; ++s) {
+                            const int64_t f = (task * NS + s) * fpw + (lane >> gsh);
+                            const int at = (fl & MF_VIA_PS)   ? gbase + pfield(stv[s].ps, op.sh_src)
+                                           : (fl & MF_VIA_PU) ? gbase + pfield(stv[s].pu, op.sh_src)
+                                                              : lane;
+                            uint32_t *dst = P.pfx + f * P.pfx_fstride + gl * P.pfx_pstride + op.dst_row;
+                            for (int w = 0; w < op.cnt; ++w) {
+                                const uint32_t x = Mv[s].ld(fl & MF_SRC_LDS, op.src_row + w, at);
+                                if (f < B) dst[w] = x;
+                            }
                         }
                     }
                     break;
@@ -1309,9 +1312,12 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
 #endif
         }
         if constexpr (PFX) {  // the stage's path metrics next to its rows; no decisions to output
-            const int64_t f = task * fpw + (threadIdx.x >> __builtin_ctz(gs));
             const int gl = threadIdx.x & (gs - 1);
-            if (f < B) *(double *)(P.pfx + f * P.pfx_fstride + gl * P.pfx_pstride + P.pm_off) = stv[0].pm;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const int64_t f = (task * NS + s) * fpw + (threadIdx.x >> __builtin_ctz(gs));
+                if (f < B) *(double *)(P.pfx + f * P.pfx_fstride + gl * P.pfx_pstride + P.pm_off) = stv[s].pm;
+            }
             wave_sync();  // the rows are reused by the next task, as after the tail below
             continue;
         }
@@ -1437,7 +1443,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
 }
 
 // ---------------------------------------------------------------------------
-// Frozen prefix (SCL-LUT in pre-mode): lut_fast_kernel<KIND, 1, false, false, true>.  Up to the first information leaf
+// Frozen prefix (SCL-LUT in pre-mode): lut_fast_kernel<KIND, NS, false, false, true>.  Up to the first information leaf
 // every path of a frame holds the same rows -- path 0 is the only one with a
 // finite metric and all decisions are frozen zeros -- yet the decode kernel
 // would compute them L times (SCLLUTDecoder.cpp:62-104 before the first fork).
@@ -1450,7 +1456,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
 // prefix's metric.  The metric is accumulated by the same code in the same
 // leaf order, so the doubles are identical.
 // ---------------------------------------------------------------------------
-#define lut_prefix_kernel(KIND) lut_fast_kernel<KIND, 1, false, false, true>
+#define lut_prefix_kernel(KIND, NS) lut_fast_kernel<KIND, NS, false, false, true>
 
 #ifndef QPD_FAST_TEMPLATES_ONLY  // qpd_fast_fscl.hip: the decode kernel templates only
 // ---------------------------------------------------------------------------
