@@ -93,11 +93,12 @@ struct qpd_decoder {
     int pfx_nops = 0;    // stage 1 (one path per frame); 0: no split
     int pfx2_nops = 0;   // stage 2 (<= 4 live paths); 0: the decode kernel resumes from stage 1
     int pfx_sets = 1;    // frame sets per wave of the prefix stages (QPD_PFX_SETS)
+    int pfx1_rec = 0, pfx1_pm = 0;  // stage 1: words per record, metric word in it
     int pfx2_rec = 0, pfx2_pm = 0;  // stage 2: words per path record, metric word in it
-    DeviceBuf pfx2_buf;  // stage 2's records: 4 paths x pfx2_rec words per frame
-    size_t pfx2_cap = 0;
-    std::vector<qpd::MOp> xin_ops;  // the decode ops' stage-2 imports, patched with pfx2_buf's address
-    const void *xin_at = nullptr;   // the address the device copies hold
+    DeviceBuf pfx1_buf, pfx2_buf;   // the stages' records (interleaved, see FastPlan::pfx)
+    size_t pfx1_cap = 0, pfx2_cap = 0;
+    std::vector<qpd::MOp> pfx_ops_host, main_ops_host;  // host copies of the split schedule (patch_imports)
+    const void *xin_at[2] = {nullptr, nullptr};         // the buffer addresses the device copies hold
     std::vector<Op> ops_host;
     DeviceBuf lut_f, f_base, lut_g, g_base, vcl, ops, info_pos, scratch, err;
     DeviceBuf r_f, r_g, q_bnd, q_rec, bnd_off, bnd_len, rec_off, rec_len;  // float-domain re-quantizers
@@ -588,8 +589,8 @@ void op_rows(const qpd::MOp &m, Fn &&acc) {
 // writing them (live-in) and begins with OP_IMPORT of its predecessor's.
 struct PrefixPlan {
     std::vector<qpd::MOp> st1, st2, rest;
+    int rec1 = 0, pm1 = 0;  // stage 1: words per record, metric word in it
     int rec2 = 0, pm2 = 0;  // stage 2: words per path record, metric word in it
-    int nimp2 = 0;          // the decode ops' first nimp2 ops: stage-2 imports (MF_XBUF)
 };
 
 bool is_fork(const qpd::MOp &m) {
@@ -651,45 +652,49 @@ qpd::MOp blank_op(int type) {
     return m;
 }
 
-bool plan_prefix(const std::vector<qpd::MOp> &ops, const FastOwner &own, int N, int L, PrefixPlan &pp) {
+bool plan_prefix(const std::vector<qpd::MOp> &ops, const FastOwner &own, int L, PrefixPlan &pp) {
     using namespace qpd;
     size_t s1 = 0;
     while (s1 < ops.size() && !is_fork(ops[s1])) ++s1;
     if (s1 == 0 || s1 == ops.size()) return false;
-    // stage 1 -> pre-pass row quarter [3N/16, N/4 - 2) + the metric at N/4 - 2: S words
-    // (computed), U / R words are zeros (every decision of the prefix is a frozen 0)
+    // stage 1 -> one-path records (geometry G = 6, PS = 0): S words (computed) and the
+    // metric; U / R words are zeros (every decision of the prefix is a frozen 0)
     std::vector<char> live1[2];
     if (!live_in(ops, s1, own, live1)) return false;
-    const int pm1 = N / 4 - 2;
-    int at = 3 * (N / 16);
     std::vector<MOp> imp1, exp1;
-    bool fits = true;
+    int w1 = 0;
     live_runs(live1, own, [&](int sp, int r, int cnt, int slot, int) {
         MOp m = blank_op(OP_IMPORT);
         m.dst_row = r;
         m.cnt = cnt;
         m.flags = sp ? MF_DST_LDS : 0;
         if (slot == 1) {
-            if (at + cnt > pm1) fits = false;
-            m.flags |= MF_PRE;
-            m.src_row = at;
+            m.flags |= MF_XBUF;
+            m.src_row = w1;
             MOp x = blank_op(OP_EXPORT);
             x.flags = sp ? MF_SRC_LDS : 0;
             x.src_row = r;
-            x.dst_row = at;
+            x.dst_row = w1;
             x.cnt = cnt;
             exp1.push_back(x);
-            at += cnt;
+            w1 += cnt;
         } else {
             m.flags |= MF_ZERO;
         }
         imp1.push_back(m);
     });
-    if (!fits) return false;
+    pp.pm1 = w1;
+    pp.rec1 = w1 + 2;
     MOp pm = blank_op(OP_IMPORT);
-    pm.flags = MF_PRE | MF_PM;
-    pm.src_row = pm1;
+    pm.flags = MF_XBUF | MF_PM;
+    pm.src_row = pp.pm1;
     imp1.insert(imp1.begin(), pm);
+    for (MOp &m : imp1) {  // record words, geometry and live paths; the address is patched per buffer
+        m.tab = pp.rec1;
+        m.vrow = 6;
+        m.tab2 = 1;
+        m.node = 1;  // buffer: stage 1's
+    }
     pp.st1.assign(ops.begin(), ops.begin() + s1);
     pp.st1.insert(pp.st1.end(), exp1.begin(), exp1.end());
     // stage 2 (L > 4): up to the op with the third information leaf
@@ -701,10 +706,12 @@ bool plan_prefix(const std::vector<qpd::MOp> &ops, const FastOwner &own, int N, 
         pp.rest.insert(pp.rest.end(), ops.begin() + s1, ops.end());
         return true;
     }
+    // stage 2 -> four-path records (G = 4, PS = 2): every live word, read through the
+    // lineage's pointer of its depth, and the metric
     std::vector<MOp> imp2, exp2;
     int w2 = 0;
     live_runs(live2, own, [&](int sp, int r, int cnt, int slot, int dd) {
-        MOp x = blank_op(OP_EXPORT);  // read through the lineage's pointer of that depth
+        MOp x = blank_op(OP_EXPORT);
         x.flags = (sp ? MF_SRC_LDS : 0) | (slot == 1 ? MF_VIA_PS : slot == 2 ? MF_VIA_PU : 0);
         x.sh_src = 4 * dd;
         x.src_row = r;
@@ -719,24 +726,61 @@ bool plan_prefix(const std::vector<qpd::MOp> &ops, const FastOwner &own, int N, 
         imp2.push_back(m);
         w2 += cnt;
     });
-    pp.pm2 = (w2 + 1) & ~1;
-    pp.rec2 = pp.pm2 + 2;
+    pp.pm2 = w2;
+    pp.rec2 = w2 + 2;
     MOp pm2 = blank_op(OP_IMPORT);
     pm2.flags = MF_XBUF | MF_PM;
     pm2.src_row = pp.pm2;
     imp2.insert(imp2.begin(), pm2);
-    for (MOp &m : imp2) {  // record strides (words) and live paths; the address is patched per buffer
-        m.tab = 4 * pp.rec2;
-        m.vrow = pp.rec2;
+    for (MOp &m : imp2) {
+        m.tab = pp.rec2;
+        m.vrow = 4 | (2 << 8);
         m.tab2 = 4;
+        m.node = 2;  // buffer: stage 2's
     }
-    pp.nimp2 = (int)imp2.size();
     pp.st2 = imp1;
     pp.st2.insert(pp.st2.end(), ops.begin() + s1, ops.begin() + s2);
     pp.st2.insert(pp.st2.end(), exp2.begin(), exp2.end());
     pp.rest = imp2;
     pp.rest.insert(pp.rest.end(), ops.begin() + s2, ops.end());
     return true;
+}
+
+// Point the import ops of a prefix-split schedule at the stage buffers (op.node: 1 / 2),
+// on the launch stream, when a buffer moved.
+int patch_imports(qpd_decoder *d, hipStream_t st) {
+    const void *b1 = d->pfx1_buf.p, *b2 = d->pfx2_buf.p;
+    if (d->xin_at[0] == b1 && d->xin_at[1] == b2) return QPD_OK;
+    auto patch = [&](std::vector<qpd::MOp> &v) {
+        for (qpd::MOp &m : v)
+            if (m.type == qpd::OP_IMPORT && (m.flags & qpd::MF_XBUF)) {
+                const uint64_t a = (uint64_t)(uintptr_t)(m.node == 2 ? b2 : b1);
+                m.u_row = (int32_t)(uint32_t)a;
+                m.r_row = (int32_t)(uint32_t)(a >> 32);
+            }
+    };
+    patch(d->pfx_ops_host);
+    patch(d->main_ops_host);
+    QPD_HIP(hipMemcpyAsync(d->pfx_mops.p, d->pfx_ops_host.data(), d->pfx_ops_host.size() * sizeof(qpd::MOp),
+                           hipMemcpyHostToDevice, st));
+    QPD_HIP(hipMemcpyAsync(d->mops.p, d->main_ops_host.data(), d->main_ops_host.size() * sizeof(qpd::MOp),
+                           hipMemcpyHostToDevice, st));
+    d->xin_at[0] = b1;
+    d->xin_at[1] = b2;
+    return QPD_OK;
+}
+
+// A stage's record buffer for Bc frames (rounded up to whole 64-frame groups), grown on demand.
+int ensure_records(DeviceBuf &b, size_t &cap, int64_t Bc, int rec, int paths) {
+    const size_t need = (size_t)((Bc + 63) / 64 * 64) * (size_t)rec * paths * sizeof(uint32_t);
+    if (cap >= need) return QPD_OK;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    cap = 0;
+    const hipError_t e = hipMalloc(&b.p, need);
+    if (e != hipSuccess) return fail(QPD_E_DEVICE, std::string("prefix records hipMalloc: ") + hipGetErrorString(e));
+    cap = need;
+    return QPD_OK;
 }
 
 #ifndef QPD_DEFAULT_SETS
@@ -935,7 +979,6 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     // FastSCL's R0 / REP nodes already take most of the prefix (4 ops of the bench
     // code; the one-stage split measured -3 % there, profiles/r03ab_*).
     PrefixPlan pp;
-    F.pm_off = -1;
     if (Ly.pre && d->L > 1 && c->kind == QPD_SCL_LUT && !getenv("QPD_NO_PFX")) {
         FastOwner own;
         for (int dd = 0; dd <= n; ++dd)
@@ -943,7 +986,7 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
                 const int b = sl == 0 ? Ly.R[dd] : sl == 1 ? Ly.S[dd] : Ly.U[dd];
                 own.add(Ly.lds(dd), b, use[sl][dd] ? rows_of(sl, dd) : 0, sl == 0 ? 0 : sl == 1 ? 1 : 2, dd);
             }
-        if (plan_prefix(mops, own, N, d->L, pp)) mops.swap(pp.rest);
+        if (plan_prefix(mops, own, d->L, pp)) mops.swap(pp.rest);
     }
     place_syncs(pp.st1, true);
     place_syncs(pp.st2, true);
@@ -952,14 +995,16 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     d->pfx_sets = std::min(d->sets, 2);
     if (const char *e = getenv("QPD_PFX_SETS")) d->pfx_sets = std::min(d->sets, std::max(1, atoi(e)));
     d->pfx2_nops = (int)pp.st2.size();
+    d->pfx1_rec = pp.rec1;
+    d->pfx1_pm = pp.pm1;
     d->pfx2_rec = pp.rec2;
     d->pfx2_pm = pp.pm2;
-    d->xin_ops.assign(mops.begin(), mops.begin() + (d->pfx2_nops > 0 ? pp.nimp2 : 0));
-    std::vector<qpd::MOp> allp = pp.st1;  // one device array: stage 1, then stage 2
-    allp.insert(allp.end(), pp.st2.begin(), pp.st2.end());
-    if (!allp.empty()) {
-        int rc = upload(d->pfx_mops, allp.data(), allp.size(), d->hs);
+    d->pfx_ops_host = pp.st1;  // one device array: stage 1, then stage 2
+    d->pfx_ops_host.insert(d->pfx_ops_host.end(), pp.st2.begin(), pp.st2.end());
+    if (!d->pfx_ops_host.empty()) {
+        int rc = upload(d->pfx_mops, d->pfx_ops_host.data(), d->pfx_ops_host.size(), d->hs);
         if (rc) return rc;
+        d->main_ops_host = mops;  // the import ops get the record buffers' addresses (patch_imports)
     }
     for (const qpd::MOp &m : mops)  // R1 nodes the register/LDS argsort cannot take
         if (c->kind == QPD_FASTSCL_LUT && m.type == qpd::OP_R1 && m.cnt > qpd::stl::kThreshold && !(m.flags & qpd::MF_R1_LDS))
@@ -1401,52 +1446,36 @@ int decode_pre_rows(qpd_decoder *d, const uint32_t *rows, int64_t Bc, uint8_t *o
     qpd::FastPlan fp = d->fplan;
     fp.in_vec = 1;
     fp.in_shift = fp.n - 2;
-    if (d->pfx_nops > 0) {  // stage 1: the frozen prefix once per frame, into the rows' free quarter
-        qpd::FastPlan pp = fp;
+    if (d->pfx_nops > 0) {  // the frozen-prefix stages, then the decode
+        int rc = ensure_records(d->pfx1_buf, d->pfx1_cap, Bc, d->pfx1_rec, 1);
+        if (!rc && d->pfx2_nops > 0) rc = ensure_records(d->pfx2_buf, d->pfx2_cap, Bc, d->pfx2_rec, 4);
+        if (!rc) rc = patch_imports(d, st);
+        if (rc) return rc;
+        qpd::FastPlan pp = fp;  // stage 1: one path per frame
         pp.ops = (const qpd::MOp *)d->pfx_mops.p;
         pp.nops = d->pfx_nops;
         pp.gs = 1;
         pp.fpw = 64;
         pp.L = 1;
-        pp.pfx = const_cast<uint32_t *>(rows);
-        pp.pfx_fstride = fp.N / 4;
-        pp.pfx_pstride = 0;
-        pp.pm_off = fp.N / 4 - 2;
-        const int rc = fast_launch(d, pp, (const int32_t *)rows, Bc, nullptr, st, true);
+        pp.pfx = (uint32_t *)d->pfx1_buf.p;
+        pp.pfx_rec = d->pfx1_rec;
+        pp.pfx_geo = 6;
+        pp.pm_off = d->pfx1_pm;
+        rc = fast_launch(d, pp, (const int32_t *)rows, Bc, nullptr, st, true);
         if (rc) return rc;
-    }
-    if (d->pfx2_nops > 0) {  // stage 2: <= 4 live paths, L = 4, into per-path records
-        const size_t need = (size_t)Bc * 4 * d->pfx2_rec * sizeof(uint32_t);
-        if (d->pfx2_cap < need) {
-            if (d->pfx2_buf.p) (void)hipFree(d->pfx2_buf.p);
-            d->pfx2_buf.p = nullptr;
-            d->pfx2_cap = 0;
-            const hipError_t e = hipMalloc(&d->pfx2_buf.p, need);
-            if (e != hipSuccess) return fail(QPD_E_DEVICE, std::string("prefix records hipMalloc: ") + hipGetErrorString(e));
-            d->pfx2_cap = need;
+        if (d->pfx2_nops > 0) {  // stage 2: <= 4 live paths, L = 4
+            pp.ops = (const qpd::MOp *)d->pfx_mops.p + d->pfx_nops;
+            pp.nops = d->pfx2_nops;
+            pp.gs = 4;
+            pp.fpw = 16;
+            pp.L = 4;
+            pp.pfx = (uint32_t *)d->pfx2_buf.p;
+            pp.pfx_rec = d->pfx2_rec;
+            pp.pfx_geo = 4 | (2 << 8);
+            pp.pm_off = d->pfx2_pm;
+            rc = fast_launch(d, pp, (const int32_t *)rows, Bc, nullptr, st, true);
+            if (rc) return rc;
         }
-        qpd::FastPlan pp = fp;
-        pp.ops = (const qpd::MOp *)d->pfx_mops.p + d->pfx_nops;
-        pp.nops = d->pfx2_nops;
-        pp.gs = 4;
-        pp.fpw = 16;
-        pp.L = 4;
-        pp.pfx = (uint32_t *)d->pfx2_buf.p;
-        pp.pfx_fstride = 4 * d->pfx2_rec;
-        pp.pfx_pstride = d->pfx2_rec;
-        pp.pm_off = d->pfx2_pm;
-        if (d->xin_at != d->pfx2_buf.p) {  // the decode's import ops carry the records' address
-            const uint64_t a = (uint64_t)(uintptr_t)d->pfx2_buf.p;
-            for (qpd::MOp &m : d->xin_ops) {
-                m.u_row = (int32_t)(uint32_t)a;
-                m.r_row = (int32_t)(uint32_t)(a >> 32);
-            }
-            QPD_HIP(hipMemcpyAsync(d->mops.p, d->xin_ops.data(), d->xin_ops.size() * sizeof(qpd::MOp),
-                                   hipMemcpyHostToDevice, st));
-            d->xin_at = d->pfx2_buf.p;
-        }
-        const int rc = fast_launch(d, pp, (const int32_t *)rows, Bc, nullptr, st, true);
-        if (rc) return rc;
     }
     return fast_launch(d, fp, (const int32_t *)rows, Bc, out, st);
 }

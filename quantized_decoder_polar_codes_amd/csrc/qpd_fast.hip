@@ -51,11 +51,11 @@ enum MopFlag : int32_t {
     MF_BCOMB = 4096,  // right BOT3 that also runs its parent's combine (dst = U/R[n-4])
     MF_VUNI = 8192,   // special node whose elements share one quanta row (v <= 16): quanta and
                       //   R1 ranks are looked up in a register row instead of gathered per element
-    MF_ZERO = 16384,  // OP_IMPORT: zero rows (partial sums of the frozen prefix) instead of pre-row words
-    MF_PM = 32768,    // OP_IMPORT: the path metric (a double at word src_row of the source record)
+    MF_ZERO = 16384,  // OP_IMPORT: zero rows (partial sums of the frozen prefix) instead of record words
+    MF_PM = 32768,    // OP_IMPORT: the path metric (a double in words src_row, src_row + 1 of the record)
     MF_VIA_PS = 65536,   // OP_EXPORT: the row is read through the path's S pointer of depth sh_src / 4
     MF_VIA_PU = 131072,  //   ... or its U pointer (else the lane's own row: R rows)
-    MF_XBUF = 262144,    // OP_IMPORT: from the stage-2 per-path records (address in the op record), not the pre-pass row
+    MF_XBUF = 262144,    // OP_IMPORT: from a prefix stage's records (address and layout in the op record)
 };
 
 struct MOp {
@@ -96,16 +96,17 @@ struct FastPlan {
     int32_t *err;
     uint32_t *task_ctr;           // QPD_DYN task queue: tasks taken (never reset; see wave_take)
     uint32_t task_base;           // per launch: the counter's value when this launch's takes begin
-    // Frozen-prefix stages (lut_prefix_kernel).  A stage writes, per frame f and path
-    // gl, its live rows (OP_EXPORT) and metric (word pm_off) to the record at
-    // pfx + f * pfx_fstride + gl * pfx_pstride: stage 1 (one path) into the free last
-    // quarter of the pre-pass row, stage 2 (live paths <= 4) into a buffer of its own.
-    // OP_IMPORT with MF_XBUF reads stage-2 records back; the buffer address and strides
-    // ride in the op record (u_row | r_row << 32, tab, vrow, tab2 live paths), not in
-    // the plan: plan fields the decode loop reads cost it SGPRs (spill 149 -> 158).
+    // Frozen-prefix stages (lut_prefix_kernel).  A stage writes, per frame f and path p,
+    // its live rows (OP_EXPORT) and metric (two words from pm_off) as a record of pfx_rec
+    // words in a buffer of its own, interleaved so that the 64 lanes of a wave store 64
+    // consecutive words: word w of (f, p) at ((f >> G) * pfx_rec + w) * 64 + (f mod 2^G) *
+    // 2^PS + p, pfx_geo = G | PS << 8 (2^G frames of 2^PS paths per 64 words; stage 1:
+    // G = 6, PS = 0; stage 2: G = 4, PS = 2).  OP_IMPORT (MF_XBUF) reads records back with
+    // the buffer address, record words, geometry and live paths in the op record (u_row |
+    // r_row << 32, tab, vrow, tab2), not in the plan: plan fields the decode loop reads
+    // cost it SGPRs (spill 149 -> 158).
     uint32_t *pfx;
-    int64_t pfx_fstride;
-    int32_t pfx_pstride, pm_off;
+    int32_t pfx_rec, pfx_geo, pm_off;
 };
 
 // Timing experiments only (wrong results): 0 = every op reads node 0's
@@ -1247,23 +1248,27 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
                     break;
                 }
                 case OP_IMPORT:
-                    if constexpr (KIND == K_SCL_LUT) {  // a frozen-prefix stage's results (lut_prefix_kernel)
-                        const bool xb = fl & MF_XBUF;
-                        const int live = xb ? op.tab2 : 1;
+                    if constexpr (KIND == K_SCL_LUT) {  // a frozen-prefix stage's records (lut_prefix_kernel)
+                        const int live = op.tab2;
 #pragma unroll
                         for (int s = 0; s < NS; ++s) {
-                            const uint32_t *src = (const uint32_t *)yv[s];
-                            if (xb) {  // the record of this lane's path (dead paths: path 0's)
-                                int64_t f = (task * NS + s) * fpw + (lane >> gsh);
-                                if (f >= B) f = B - 1;
-                                const uint32_t *base = (const uint32_t *)(((uint64_t)(uint32_t)op.r_row << 32) | (uint32_t)op.u_row);
-                                src = base + f * op.tab + (gl < live ? gl : 0) * op.vrow;
+                            const bool dl = fl & MF_DST_LDS;
+                            if (fl & MF_ZERO) {  // the prefix's partial sums: frozen zeros
+                                for (int w = 0; w < op.cnt; ++w) Mv[s].st(dl, op.dst_row + w, lane, 0u);
+                                continue;
                             }
+                            int64_t f = (task * NS + s) * fpw + (lane >> gsh);
+                            if (f >= B) f = B - 1;
+                            const int G = op.vrow & 255;
+                            // the record of this lane's path (dead paths: path 0's)
+                            const uint32_t *src = (const uint32_t *)(((uint64_t)(uint32_t)op.r_row << 32) | (uint32_t)op.u_row) +
+                                                  (((f >> G) * op.tab) << 6) + ((f & ((1 << G) - 1)) << (op.vrow >> 8)) +
+                                                  (gl < live ? gl : 0);
                             if (fl & MF_PM) {
-                                stv[s].pm = gl < live ? *(const double *)(src + op.src_row) : kInf;
+                                const uint64_t b = (uint64_t)src[op.src_row << 6] | ((uint64_t)src[(op.src_row + 1) << 6] << 32);
+                                stv[s].pm = gl < live ? __builtin_bit_cast(double, b) : kInf;
                             } else {  // live rows into every path's own column
-                                const bool dl = fl & MF_DST_LDS, z = fl & MF_ZERO;
-                                for (int w = 0; w < op.cnt; ++w) Mv[s].st(dl, op.dst_row + w, lane, z ? 0u : src[op.src_row + w]);
+                                for (int w = 0; w < op.cnt; ++w) Mv[s].st(dl, op.dst_row + w, lane, src[(op.src_row + w) << 6]);
                             }
                         }
                     }
@@ -1276,10 +1281,11 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
                             const int at = (fl & MF_VIA_PS)   ? gbase + pfield(stv[s].ps, op.sh_src)
                                            : (fl & MF_VIA_PU) ? gbase + pfield(stv[s].pu, op.sh_src)
                                                               : lane;
-                            uint32_t *dst = P.pfx + f * P.pfx_fstride + gl * P.pfx_pstride + op.dst_row;
+                            const int G = P.pfx_geo & 255;
+                            uint32_t *dst = P.pfx + (((f >> G) * P.pfx_rec) << 6) + ((f & ((1 << G) - 1)) << (P.pfx_geo >> 8)) + gl;
                             for (int w = 0; w < op.cnt; ++w) {
                                 const uint32_t x = Mv[s].ld(fl & MF_SRC_LDS, op.src_row + w, at);
-                                if (f < B) dst[w] = x;
+                                if (f < B) dst[(op.dst_row + w) << 6] = x;
                             }
                         }
                     }
@@ -1316,7 +1322,13 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
 #pragma unroll
             for (int s = 0; s < NS; ++s) {
                 const int64_t f = (task * NS + s) * fpw + (threadIdx.x >> __builtin_ctz(gs));
-                if (f < B) *(double *)(P.pfx + f * P.pfx_fstride + gl * P.pfx_pstride + P.pm_off) = stv[s].pm;
+                const int G = P.pfx_geo & 255;
+                uint32_t *dst = P.pfx + (((f >> G) * P.pfx_rec) << 6) + ((f & ((1 << G) - 1)) << (P.pfx_geo >> 8)) + gl;
+                const uint64_t b = __builtin_bit_cast(uint64_t, stv[s].pm);
+                if (f < B) {
+                    dst[P.pm_off << 6] = (uint32_t)b;
+                    dst[(P.pm_off + 1) << 6] = (uint32_t)(b >> 32);
+                }
             }
             wave_sync();  // the rows are reused by the next task, as after the tail below
             continue;
