@@ -31,8 +31,8 @@
 namespace qpd {
 
 constexpr int OP_BOT3 = 9;    // fused bottom subtree of height 3 (fast engine only)
-constexpr int OP_IMPORT = 10; // frozen-prefix split (see lut_prefix_kernel): rows from the pre-pass row / zeros
-constexpr int OP_EXPORT = 11; // lut_prefix_kernel only: rows into the pre-pass row's free quarter
+constexpr int OP_IMPORT = 10; // frozen-prefix stages (see lut_prefix_kernel): rows / metric from a stage's records, or zeros
+constexpr int OP_EXPORT = 11; // lut_prefix_kernel only: live rows into the stage's records (FastPlan::pfx)
 
 enum MopFlag : int32_t {
     MF_SRC_LDS = 1,   // S[d] in LDS

@@ -4,7 +4,7 @@ decode kernel resumes from the exported rows and path metric.  The bits must
 equal the oracle's and the unsplit kernel's (QPD_NO_PFX=1) on every input:
   * PW codes at the bench size (split present) and odd batch sizes;
   * codes whose first bit is information (a prefix of f ops only) or whose
-    live rows do not fit the pre-pass row (the split is refused);
+    prefix is most of the schedule;
   * CRC-aided kinds, whose tail checks every path's CRC.
 """
 import numpy as np
@@ -88,11 +88,10 @@ def test_prefix_equals_unsplit(kind, N, K, L, qpd, monkeypatch):
 
 
 @pytest.mark.parametrize("N,K", [(64, 64), (1024, 1024), (1024, 16)])
-def test_prefix_refused_or_exact(N, K, qpd, oracle_mod, monkeypatch):
+def test_prefix_edge_codes_exact(N, K, qpd, oracle_mod, monkeypatch):
     """Every bit information (K = N: the prefix is only the f ops down to the
-    first leaf) or a long prefix (K = 16 of 1024: the live rows may reach past
-    the pre-pass row's free quarter and the split is refused): whatever the
-    plan chose, the bits are the oracle's."""
+    first leaf) or a long prefix (K = 16 of 1024: stage 1 runs most of the
+    schedule): whatever the plan chose, the bits are the oracle's."""
     fm, nt = _code(N, K)
     p = _tables(N, 31 + K)
     sym = np.random.default_rng(K).integers(0, 16, size=(40, N), dtype=np.int32)
