@@ -27,8 +27,8 @@ BER/BLER plus the end-to-end rate (generate + decode + count).
 
 Rank 0 prints one JSON line (contract in the task statement), including
 `roofline` for the decode kernel (HIP events around each of its launches on
-the launch stream; on-chip bytes against the LDS peak probed on this GPU) and
-`cpu_baseline` (the reference decoder compiled from its sources, oracle/_ref,
+the launch stream; on-chip bytes against the guide's aggregate LDS rate) and
+`cpu_baseline` + `parity_sample` (the reference decoder compiled from its sources, oracle/_ref,
 one worker process per host core of this GPU's CPU share, over a bounded
 sample of the same frames).
 """
@@ -50,7 +50,6 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 GUIDE_LDS_B32_GBS = 75000.0  # MI355X_MICROARCH.md §LDS: aggregate ds_read_b32, every CU streaming
 GUIDE_LDS_B64_GBS = 150000.0  # ... ds_read_b64 / b128
-LOOKUPS_PER_FRAME = 81920  # L*N*log2(N) LUT lookups at N=1024, L=8
 ONCHIP_BYTES_PER_LOOKUP = 4  # 2 operand symbols + 1 table byte + 1 result byte
 METRIC = "decoded frames/sec (N=1024, SCL-LUT L=8, Q=16) at 1/2/4/8 GPUs; BER match"
 KINDS = ["SC-LUT", "SCL-LUT", "FastSC-LUT", "FastSCL-LUT", "CA-SCL-LUT", "CA-FastSCL-LUT"]
@@ -277,12 +276,15 @@ def _counters(args, frames):
 def roofline(args, dec, kt, frames, calls):
     """Roofline of the dominant kernel (lut_fast_kernel; generic_decode_kernel
     on the generic engine).  achieved = SURVEY.md §8(d)'s algorithmic on-chip
-    bytes (L*N*log2 N LUT lookups x 4 B per frame) x frames per launch (a
-    call of `frames` frames is one launch per pre-pass chunk) / the
-    kernel's average launch duration from the HIP events on its stream; peak =
-    the ds_bpermute_b32 rate probed on this GPU now (qpd_probe_lds: the
-    instruction of every table lookup).  `hbm` keeps the contract's HBM view of
-    a whole decode call (pre-pass + decode)."""
+    bytes -- the f/g table lookups the reference's traversal of this code makes
+    (qpd_info.lookups_per_path: N log2 N per path for SC/SCL, fewer where the Fast
+    decoders' special nodes skip subtrees) x L paths x 4 B per lookup -- x frames
+    per launch (a call of `frames` frames is one launch per pre-pass chunk) / the
+    kernel's average launch duration from the HIP events on its stream.  peak =
+    the guide's aggregate LDS read rate (MI355X_MICROARCH.md §LDS: ds_read_b32,
+    every CU streaming, 75 TB/s); the ds_bpermute rate probed on this GPU (the
+    instruction the lookups use) is reported beside it.  `hbm` keeps the
+    contract's HBM view of a whole decode call (pre-pass + decode)."""
     import ctypes
 
     from quantized_decoder_polar_codes_amd import _lib
@@ -294,33 +296,38 @@ def roofline(args, dec, kt, frames, calls):
     k_ms = (dec_ms + pfx_ms) / max(1, n_dec)
     call_ms = (dec_ms + pre_ms + pfx_ms) / max(1, calls)
     per_launch = frames * calls / max(1, n_dec)  # frames per decode launch
-    n = int(np.log2(args.N))
-    onchip_per_frame = args.L * args.N * n * ONCHIP_BYTES_PER_LOOKUP if "SCL" in args.kind else args.N * n * 4
+    info = dec.info()
+    paths = args.L if "SCL" in args.kind else 1
+    lookups = paths * int(info["lookups_per_path"])
+    onchip_per_frame = lookups * ONCHIP_BYTES_PER_LOOKUP
     peaks = {}
     for name, op in (("ds_bpermute_b32", _lib.QPD_PROBE_BPERMUTE), ("ds_read_b32", _lib.QPD_PROBE_READ_B32),
                      ("ds_read_b64", _lib.QPD_PROBE_READ_B64)):
         g = ctypes.c_double()
         _lib.check(_lib.load().qpd_probe_lds(dec.device, op, ctypes.byref(g)))
         peaks[name] = g.value
-    peak = peaks["ds_bpermute_b32"]
+    peak = GUIDE_LDS_B32_GBS
     achieved = onchip_per_frame * per_launch / (k_ms * 1e-3) / 1e9
     hbm_bytes = frames * (args.N * 4 + dec.out_bits)  # int32 symbols in, uint8 bits out
     rec = _counters(args, frames)
-    kname = "lut_fast_kernel" if dec.info()["engine"] == 2 else "generic_decode_kernel"
+    kname = "lut_fast_kernel" if info["engine"] == 2 else "generic_decode_kernel"
     kc = (rec or {}).get("kernels", {}).get(kname, {})
     out = {"bound": "lds", "achieved": achieved, "peak": peak, "unit": "GB/s", "frac": achieved / peak,
+           "peak_source": "MI355X_MICROARCH.md §LDS: aggregate ds_read_b32 with every CU streaming (75 TB/s)",
            "traffic": kc.get("traffic"), "kernel": kname, "kernel_ms": dec_ms / max(1, n_dec), "launches": n_dec,
            # frozen-prefix stages (lut_prefix_kernel): their summed time per decode launch
            "prefix_kernel_ms": pfx_ms / max(1, n_dec) if n_pfx else None, "prefix_launches": n_pfx,
            "achieved_over": "lut_fast_kernel + its lut_prefix_kernel stages per launch" if n_pfx else kname,
            "algorithmic_bytes_per_launch": onchip_per_frame * per_launch,
-           "algorithmic": f"{onchip_per_frame} B/frame on-chip (SURVEY.md §8(d)) x {per_launch:.0f} frames per launch",
-           "peak_probe": peaks, "lds_hit": kc.get("lds_hit"),
-           # the guide's aggregate LDS rates (MI355X_MICROARCH.md §LDS, every CU streaming) beside the probe:
+           "lookups_per_frame": lookups,
+           "algorithmic": f"{lookups} f/g table lookups per frame ({paths} path(s) x {info['lookups_per_path']}, the "
+                          f"reference traversal of this code) x {ONCHIP_BYTES_PER_LOOKUP} B (SURVEY.md §8(d)) x "
+                          f"{per_launch:.0f} frames per launch",
            # the lookups are ds_bpermute (a cross-lane crossbar read, ~40 % of ds_read_b32 when probed);
            # LDS-resident tables read with ds_read_b32/_b64 measured 5 % slower (profiles/r03k_ab_lds_tables.txt)
+           "peak_probe": peaks, "frac_vs_probed_ds_bpermute": achieved / peaks["ds_bpermute_b32"],
            "peak_guide": {"ds_read_b32": GUIDE_LDS_B32_GBS, "ds_read_b64": GUIDE_LDS_B64_GBS},
-           "frac_vs_guide_ds_read_b32": achieved / GUIDE_LDS_B32_GBS,
+           "lds_hit": kc.get("lds_hit"),
            "traffic_bytes_per_frame": (kc.get("traffic") / per_launch) if kc.get("traffic") else None,
            "traffic_note": "HBM-side bytes per launch of this kernel, 2 x FETCH_SIZE + WRITE_SIZE from separate "
                            "rocprofv3 --pmc passes (profiles/counters.json via tools/counters.py)",
@@ -479,8 +486,11 @@ def cpu_baseline(args, packed, fm, nt, sym, seconds, workers, A):
             "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
             "cores_note": f"{workers} worker processes = this GPU's CPU share (OMP_NUM_THREADS on the GPU box); "
                           f"the machine shows {os.cpu_count()} CPUs shared by its 8 GPUs",
-            "build": "reference decoder sources compiled by oracle/build_ref.sh: g++ -O3 -DNDEBUG, the reference's "
-                     "Release flags without its -march=native (built in the container, run on this host)",
+            "build": ("reference decoder sources compiled by oracle/build_ref.sh: g++ -O3 -DNDEBUG, the reference's "
+                      "Release flags without its -march=native (built in the container, run on this host)")
+            if kind == "reference" else
+            ("the oracle's C++ restatement of the reference (oracle/qpd_oracle.cpp, built by oracle/Makefile; "
+             "oracle/_ref was not present on this host)"),
             "sample": f"{total} frames of the same workload (rank 0's first frames), {workers} worker processes x "
                       f"one decode() call per frame, {wall:.1f} s"}, outs
 
@@ -514,6 +524,22 @@ def rank_job(args, ctx, make_workload):
     return res, wl
 
 
+def parity_and_baseline(args, wl, res):
+    """Rank 0: the reference CPU decoder on a bounded sample of this rank's
+    resident frames (cpu_baseline) and the GPU bits of the same frames against
+    it (parity_sample).  Runs after the timed steps at any world size, so every
+    line of a 1..8-GPU scaling run carries its bit-exactness check."""
+    workers = args.cpu_workers or min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+    sample = wl.sym[: 1 << 15].cpu().numpy()
+    cb, parts = cpu_baseline(args, wl.packed, wl.fm, wl.nt, sample, args.cpu_baseline_seconds, max(1, workers),
+                             wl.dec.out_bits)
+    res["cpu_baseline"] = cb
+    gpu_out = wl.dec.decode_batch(wl.sym[: 1 << 15]).cpu().numpy()
+    ok = all(np.array_equal(gpu_out[o:o + len(r)], r) for o, r in parts)
+    res["parity_sample"] = {"frames": int(sum(len(r) for _, r in parts)), "bit_exact_vs_" + cb["kind"]: bool(ok),
+                            "rank": 0, "frames_from": "rank 0's first resident frames (global ids 0..)"}
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
@@ -522,6 +548,7 @@ def main(argv=None):
     import torch
     import torch.distributed as dist
 
+    launched = "WORLD_SIZE" in os.environ  # under torch.distributed.run (the driver's N-GPU launches)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -532,7 +559,7 @@ def main(argv=None):
     devs = [int(x) for x in os.environ.get("QPD_BENCH_DEVICES", "").split(",") if x.strip()]
     torch.cuda.set_device(devs[local % len(devs)] if devs else (local if world > 1 else 0))
     group = None
-    if world > 1:
+    if launched:  # every torchrun launch, world size 1 included, reduces over a process group
         dist.init_process_group(os.environ.get("QPD_BENCH_BACKEND", "nccl"))  # "nccl" = RCCL over xGMI
         group = dist.group.WORLD
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -543,19 +570,15 @@ def main(argv=None):
                         frame0=frame0, device=dev.index, max_waves=args.max_waves, engine=args.engine)
 
     res, wl = rank_job(args, ctx, make)
-    if not args.mc_frames:
-        if res is not None and world == 1 and not args.no_cpu_baseline:
-            workers = args.cpu_workers or min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
-            sample = wl.sym[: 1 << 15].cpu().numpy()
-            cb, parts = cpu_baseline(args, wl.packed, wl.fm, wl.nt, sample, args.cpu_baseline_seconds,
-                                     max(1, workers), wl.dec.out_bits)
-            res["cpu_baseline"] = cb
-            gpu_out = wl.dec.decode_batch(wl.sym[: 1 << 15]).cpu().numpy()
-            ok = all(np.array_equal(gpu_out[o:o + len(r)], r) for o, r in parts)
-            res["parity_sample"] = {"frames": int(sum(len(r) for _, r in parts)), "bit_exact_vs_" + cb["kind"]: bool(ok)}
+    if not args.mc_frames and not args.no_cpu_baseline:
+        if res is not None:
+            parity_and_baseline(args, wl, res)
+            res["config"]["process_group"] = dist.get_backend(group) if group is not None else None
+        if group is not None:
+            dist.barrier(group=group)  # the other ranks wait for rank 0's CPU leg
     if res is not None:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if group is not None:
         dist.destroy_process_group()
 
 

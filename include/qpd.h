@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define QPD_ABI_VERSION 4
+#define QPD_ABI_VERSION 5
 
 /* Decoder kinds (the reference's class names). */
 enum qpd_kind {
@@ -296,7 +296,16 @@ typedef struct qpd_info {
     int32_t prefix_ops;       /* fast engine, list kinds: ops of the frozen prefix run
                                  once per frame by lut_prefix_kernel (0: no split);
                                  num_ops counts both parts */
+    int32_t last_engine;      /* enum qpd_ran: what decoded the handle's last decode
+                                 call (tests assert that a "GPU" case ran the kernels) */
+    int64_t lookups_per_path; /* f/g table lookups one path of one frame makes in the
+                                 reference's traversal of this code (N log2 N for the
+                                 SC/SCL kinds; fewer where special nodes skip subtrees):
+                                 the algorithmic unit of the roofline (bench.py) */
 } qpd_info;
+/* qpd_info.last_engine: no decode yet, the GPU kernels (qpd_decode*, the GPU
+ * branch of the host-buffer calls, qpd_mc_decode), or the host engine. */
+enum qpd_ran { QPD_RAN_NONE = 0, QPD_RAN_GPU = 1, QPD_RAN_HOST = 2 };
 int qpd_get_info(const qpd_decoder *dec, qpd_info *info);
 
 /*

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("QPD_LIB") or os.path.join(HERE, "libqpd.so")
  QPD_SCL_LLOYD) = range(15)
 FLOAT_KINDS = (QPD_SC_FLOAT, QPD_SCL_FLOAT, QPD_CASCL_FLOAT, QPD_FASTSC_FLOAT, QPD_FASTSCL_FLOAT, QPD_SC_UNIFORM,
                QPD_SCL_UNIFORM, QPD_SC_LLOYD, QPD_SCL_LLOYD)
-ABI_VERSION = 4
+ABI_VERSION = 5
 QPD_ENGINE_AUTO, QPD_ENGINE_GENERIC, QPD_ENGINE_FAST = range(3)
 QPD_OK, QPD_E_INVALID, QPD_E_UNSUPPORTED, QPD_E_DEVICE, QPD_E_INPUT = 0, -1, -2, -3, -4
 
@@ -46,6 +46,7 @@ EXPORTED = (
 QPD_KC_PRE, QPD_KC_DECODE, QPD_KC_MC, QPD_KC_PFX, QPD_KC_COUNT = range(5)
 QPD_PROBE_BPERMUTE, QPD_PROBE_READ_B32, QPD_PROBE_READ_B64 = range(3)
 QPD_HOST_AUTO, QPD_HOST_GPU, QPD_HOST_CPU = range(3)
+QPD_RAN_NONE, QPD_RAN_GPU, QPD_RAN_HOST = range(3)
 
 _P = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -119,6 +120,8 @@ class QpdInfo(ctypes.Structure):
         ("out_bits", _i32),
         ("host_max_frames", _i64),
         ("prefix_ops", _i32),
+        ("last_engine", _i32),
+        ("lookups_per_path", _i64),
     ]
 
 

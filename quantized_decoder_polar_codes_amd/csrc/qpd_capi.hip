@@ -82,9 +82,11 @@ struct qpd_decoder {
     bool pre = false;         // fast engine pre-mode: root_pre_kernel, then the decode on its rows
     int64_t pre_chunk = 0;    // frames per pre-pass chunk
     int64_t pre_cap = 0;      // frames pre_buf holds
+    bool pre_fell_back = false;  // an allocation of pre-pass rows failed: pre_cap is the chunk from then on
     DeviceBuf pre_buf;
     DeviceBuf mc_sym;        // qpd_mc_decode without a fused pre-pass: int32 symbols of one chunk
     int64_t mc_sym_cap = 0;  // frames mc_sym holds
+    bool mc_sym_fell_back = false;
     DevPlan plan{};
     qpd::FastPlan fplan{};
     DeviceBuf f_tab, g_tab, fscratch, mops, r1_rank, task_ctr;
@@ -131,6 +133,7 @@ struct qpd_decoder {
     std::unique_ptr<qpd_host::Engine<double>> heng_f64;
     int host_mode = QPD_HOST_AUTO;
     int64_t host_max_frames = 0;  // QPD_HOST_AUTO: batches up to this size run on the host engine
+    int last_engine = QPD_RAN_NONE;  // what served the last decode call (qpd_info.last_engine)
     // qpd_profile: HIP events around every launch, per kernel class
     bool prof = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[QPD_KC_COUNT];
@@ -979,7 +982,17 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     // FastSCL's R0 / REP nodes already take most of the prefix (4 ops of the bench
     // code; the one-stage split measured -3 % there, profiles/r03ab_*).
     PrefixPlan pp;
-    if (Ly.pre && d->L > 1 && c->kind == QPD_SCL_LUT && !getenv("QPD_NO_PFX")) {
+    // The split needs every live path metric finite: stage 2 and the decode
+    // kernel seed the dead slots with path 0's rows and +inf, where the
+    // reference holds copies of other dead paths (SCLLUTDecoder.cpp:117-144);
+    // the two agree while no live metric reaches +inf and ties with a dead one.
+    // A metric is a sum of at most N leaf quanta (row n-1), so quanta below
+    // DBL_MAX / 2N keep it finite; tables beyond that decode unsplit, exactly
+    // as the reference does with its infinities.
+    double qmax = 0.0;
+    for (size_t i = (size_t)(n - 1) * N * v; i < (size_t)n * N * v; ++i) qmax = std::max(qmax, std::fabs(c->vcl[i]));
+    const bool pm_finite = qmax <= __DBL_MAX__ / (2.0 * N);
+    if (Ly.pre && d->L > 1 && c->kind == QPD_SCL_LUT && pm_finite && !getenv("QPD_NO_PFX")) {
         FastOwner own;
         for (int dd = 0; dd <= n; ++dd)
             for (int sl = 0; sl < 3; ++sl) {
@@ -993,7 +1006,9 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     place_syncs(mops, c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT);
     d->pfx_nops = (int)pp.st1.size();
     d->pfx_sets = std::min(d->sets, 2);
-    if (const char *e = getenv("QPD_PFX_SETS")) d->pfx_sets = std::min(d->sets, std::max(1, atoi(e)));
+    // prefix_kernel() instantiates NS = 1 and 2 only: fast_launch's task count
+    // (fgroups) must use the NS the launched kernel has
+    if (const char *e = getenv("QPD_PFX_SETS")) d->pfx_sets = std::min(std::min(d->sets, 2), std::max(1, atoi(e)));
     d->pfx2_nops = (int)pp.st2.size();
     d->pfx1_rec = pp.rec1;
     d->pfx1_pm = pp.pm1;
@@ -1122,7 +1137,7 @@ int launch_generic(qpd_decoder *d, const In *in, int64_t B, uint8_t *out, int gr
 // The host engine's copy of the plan (qpd_host.hpp) and the batch size up to
 // which QPD_HOST_AUTO prefers it.  The crossover is a cost model fitted to the
 // per-call latencies measured on MI355X (tools/latency.py,
-// profiles/r03_latency.jsonl): a GPU call costs a fixed launch / copy /
+// profiles/r02_latency.jsonl, re-checked on profiles/r03af_latency.jsonl): a GPU call costs a fixed launch / copy /
 // synchronization overhead plus one wave running the whole serial schedule,
 // whatever the batch up to thousands of frames; the host engine costs its
 // per-frame work times the batch.
@@ -1134,13 +1149,14 @@ int build_host(qpd_decoder *d, const qpd_config *cfg, size_t nops) {
     else
         d->heng_f64 = std::make_unique<qpd_host::Engine<double>>(*h);
     // Per frame on the host engine ~ its lookups (N log2 N per path) plus,
-    // for lists, the forks (measured: SC-LUT N=128 4.5 us, N=1024 46 us,
-    // SCL-LUT N=1024 L=8 0.57 ms); a GPU call ~ 55 us of launches, copies
-    // and synchronization plus one wave running the serial schedule
-    // (SC-LUT N=128 0.11 ms, N=1024 0.91 ms, SCL-LUT N=1024 L=8 1.06 ms,
-    // profiles/r02_latency.jsonl) -- flat in the batch up to thousands of frames.
+    // for lists, the forks (re-fitted to the round-3 engine, profiles/
+    // r03af_latency.jsonl: SC-LUT N=128 2.8 us, N=1024 15.5 us, SCL-LUT
+    // N=1024 L=8 0.154 ms); a GPU call ~ 55 us of launches, copies and
+    // synchronization plus one wave running the serial schedule (SC-LUT N=128
+    // 0.11 ms, N=1024 0.91 ms, SCL-LUT N=1024 L=8 1.07 ms, same file) -- flat
+    // in the batch up to thousands of frames.
     const double nn = (double)h->N * h->n;
-    const double host_us = 0.004 * nn * h->L + (h->L > 1 ? 0.05 * h->L * h->N : 0.0) + 1.0;
+    const double host_us = 0.00136 * nn * h->L + (h->L > 1 ? 0.005 * h->L * h->N : 0.0) + 1.6;
     const double gpu_us = 55.0 + 0.083 * nn + (h->L > 1 ? 0.02 * nn : 0.0);
     (void)nops;
     d->host_max_frames = std::max<int64_t>(1, (int64_t)(gpu_us / host_us));
@@ -1403,6 +1419,14 @@ int qpd_get_info(const qpd_decoder *d, qpd_info *info) {
     info->lds_bytes_per_wave = d->lds_bytes;
     info->lds_from_depth = d->engine == QPD_ENGINE_FAST ? d->fplan.lds_from : -1;
     info->prefix_ops = d->engine == QPD_ENGINE_FAST ? d->pfx_nops + d->pfx2_nops : 0;
+    info->last_engine = d->last_engine;
+    // f / g ops of a node at depth d look up N >> (d + 1) symbols each; a leaf
+    // pair's two decisions one each (SCLLUTDecoder.cpp:83-89, :157-164)
+    int64_t lk = 0;
+    for (const Op &o : d->ops_host)
+        if (o.type == qpd::OP_F || o.type == qpd::OP_G) lk += d->N >> (o.d + 1);
+        else if (o.type == qpd::OP_LEAF_L || o.type == qpd::OP_LEAF_R) lk += 1;
+    info->lookups_per_path = lk;
     return QPD_OK;
 }
 
@@ -1485,10 +1509,14 @@ int decode_pre_rows(qpd_decoder *d, const uint32_t *rows, int64_t Bc, uint8_t *o
 // results).  Returns the frames the buffer holds.
 int64_t ensure_pre_rows(qpd_decoder *d, int64_t chunk, int *rc) {
     *rc = QPD_OK;
+    // after a fallback the smaller buffer is the chunk: no device-wide hipFree
+    // and failing hipMallocs on every later call
+    if (d->pre_fell_back) chunk = std::min<int64_t>(chunk, d->pre_cap);
     if (d->pre_cap >= chunk) return std::min<int64_t>(chunk, d->pre_cap);
     if (d->pre_buf.p) (void)hipFree(d->pre_buf.p);
     d->pre_buf.p = nullptr;
     d->pre_cap = 0;
+    const int64_t want = chunk;
     hipError_t e = hipErrorOutOfMemory;
     while (chunk >= 1 && (e = hipMalloc(&d->pre_buf.p, (size_t)chunk * (size_t)d->N)) != hipSuccess) {
         (void)hipGetLastError();
@@ -1499,6 +1527,7 @@ int64_t ensure_pre_rows(qpd_decoder *d, int64_t chunk, int *rc) {
         *rc = fail(QPD_E_DEVICE, std::string("pre-pass rows hipMalloc: ") + hipGetErrorString(e));
         return 0;
     }
+    d->pre_fell_back = d->pre_fell_back || e != hipSuccess || chunk < want;
     d->pre_cap = chunk;
     return chunk;
 }
@@ -1507,6 +1536,7 @@ int64_t ensure_pre_rows(qpd_decoder *d, int64_t chunk, int *rc) {
 // stream ordered).
 int decode_impl(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_out, hipStream_t st) {
     int rc = QPD_OK;
+    d->last_engine = QPD_RAN_GPU;
     if (d->engine != QPD_ENGINE_FAST) {
         const int64_t groups = (B + d->plan.fpw - 1) / d->plan.fpw;
         return launch_generic(d, d_symbols, B, d_out, (int)std::min<int64_t>(groups, d->max_waves), st);
@@ -1541,6 +1571,7 @@ int decode_impl(qpd_decoder *d, const int32_t *d_symbols, int64_t B, uint8_t *d_
 }
 
 int decode_f64_impl(qpd_decoder *d, const double *d_llr, int64_t B, uint8_t *d_out, hipStream_t st) {
+    d->last_engine = QPD_RAN_GPU;
     const int64_t groups = (B + d->plan.fpw - 1) / d->plan.fpw;
     const int grid = (int)std::min<int64_t>(groups, d->max_waves);
     return launch_generic(d, d_llr, B, d_out, grid, st);
@@ -1700,6 +1731,7 @@ static bool host_engine_takes(const qpd_decoder *d, int64_t B) {
 template <class Eng, class In>
 static int host_engine_run(qpd_decoder *d, Eng *eng, const In *h_in, int64_t B, uint8_t *h_out) {
     std::lock_guard<std::mutex> lk(d->mu);
+    d->last_engine = QPD_RAN_HOST;
     int32_t flag = 0;
     for (int64_t b = 0; b < B; ++b) flag |= eng->decode(h_in + b * d->N, h_out + b * d->out_bits);
     return flag ? input_error(flag) : QPD_OK;
@@ -1819,20 +1851,33 @@ int qpd_mc_decode(qpd_decoder *d, const qpd_mc_channel *ch, uint64_t seed, int64
         // kernel reads (fast engine in pre-mode; symbols < q <= v need no
         // range check); else int32 symbols in a buffer of its own
         const bool fused = d->engine == QPD_ENGINE_FAST && d->pre && ch->q <= d->v;
+        d->last_engine = QPD_RAN_GPU;
         int64_t chunk;
         if (fused) {
             int r0 = QPD_OK;
             chunk = ensure_pre_rows(d, std::min<int64_t>(B, d->pre_chunk), &r0);
             if (r0) return r0;
         } else {
-            chunk = std::min<int64_t>(B, (int64_t)1 << 20);
+            // int32 symbols of <= 1 GB per chunk (2^18 frames at N = 1024); halved
+            // on an allocation failure, and the smaller buffer kept from then on
+            chunk = std::min<int64_t>(B, std::max<int64_t>(1, ((int64_t)1 << 30) / ((int64_t)d->N * 4)));
+            if (d->mc_sym_fell_back) chunk = std::min(chunk, d->mc_sym_cap);
             if (d->mc_sym_cap < chunk) {
                 if (d->mc_sym.p) QPD_HIP(hipFree(d->mc_sym.p));
                 d->mc_sym.p = nullptr;
                 d->mc_sym_cap = 0;
-                QPD_HIP(hipMalloc(&d->mc_sym.p, (size_t)chunk * d->N * sizeof(int32_t)));
+                hipError_t e = hipErrorOutOfMemory;
+                const int64_t want = chunk;
+                while (chunk >= 1 && (e = hipMalloc(&d->mc_sym.p, (size_t)chunk * d->N * sizeof(int32_t))) != hipSuccess) {
+                    (void)hipGetLastError();
+                    d->mc_sym.p = nullptr;
+                    chunk /= 2;
+                }
+                if (e != hipSuccess) return fail(QPD_E_DEVICE, std::string("Monte-Carlo symbols hipMalloc: ") + hipGetErrorString(e));
+                d->mc_sym_fell_back = chunk < want;
                 d->mc_sym_cap = chunk;
             }
+            chunk = std::min(chunk, d->mc_sym_cap);
         }
         DeviceBuf &buf = fused ? d->pre_buf : d->mc_sym;
         for (int64_t f0 = 0; f0 < B; f0 += chunk) {

@@ -1457,16 +1457,25 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND 
 // ---------------------------------------------------------------------------
 // Frozen prefix (SCL-LUT in pre-mode): lut_fast_kernel<KIND, NS, false, false, true>.  Up to the first information leaf
 // every path of a frame holds the same rows -- path 0 is the only one with a
-// finite metric and all decisions are frozen zeros -- yet the decode kernel
-// would compute them L times (SCLLUTDecoder.cpp:62-104 before the first fork).
-// This kernel runs that op prefix once per frame, one lane per frame (gs = 1,
-// 64 frames per wave, the same op code and row layout), and leaves the rows
-// the rest of the schedule reads (OP_EXPORT) plus path 0's metric in the free
-// last quarter of the frame's pre-pass row.  The decode kernel then starts at
-// the first forking op: OP_IMPORT ops copy those rows into every path's own
-// column (and zero the prefix's partial-sum rows), and path 0 starts from the
-// prefix's metric.  The metric is accumulated by the same code in the same
-// leaf order, so the doubles are identical.
+// finite metric and all decisions are frozen zeros -- and until the third one
+// at most 4 paths are live, yet the decode kernel would compute all of it L
+// times (SCLLUTDecoder.cpp:62-144).  Two launches of this instantiation run
+// that part of the schedule on the same op code and row layout:
+//  * stage 1 -- the ops before the first forking op, one lane per frame (gs = 1,
+//    64 frames per set);
+//  * stage 2 -- from there to the op of the third information leaf at L = 4
+//    (gs = 4), starting from stage 1's records (OP_IMPORT, MF_XBUF).
+// Each stage ends with OP_EXPORT ops that write the rows the rest of the
+// schedule reads before writing, through each path's lineage pointers, plus
+// every path's metric, into the stage's own record buffer (d->pfx1_buf /
+// pfx2_buf), interleaved across the frames of a 64-word block (FastPlan::pfx:
+// address, record length and geometry).  The next stage or the decode kernel
+// starts at the op after the split with OP_IMPORT ops (record address and
+// layout in the op record) that copy each live path's record into its own
+// column, zero the prefix's partial-sum rows (MF_ZERO) and load the metrics
+// (MF_PM); dead slots start from path 0's rows with +inf.  The metrics are
+// accumulated by the same code in the same leaf order, so the doubles are
+// identical.
 // ---------------------------------------------------------------------------
 #define lut_prefix_kernel(KIND, NS) lut_fast_kernel<KIND, NS, false, false, true>
 

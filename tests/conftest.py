@@ -15,6 +15,23 @@ GOLDEN_DIR = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libqpd.so on cuda:0)")
+    config.addinivalue_line("markers", "host_engine: a gpu test that exercises the host engine on purpose "
+                                       "(the kernels-only fixture below leaves QPD_HOST_ENGINE alone)")
+
+
+ENGINE_NAMES = {0: "none", 1: "gpu", 2: "host"}  # qpd_info.last_engine (enum qpd_ran, include/qpd.h)
+
+
+@pytest.fixture(autouse=True)
+def _gpu_tests_run_the_kernels(request, monkeypatch):
+    """Every -m gpu test runs the HIP kernels: host-buffer calls of a few frames
+    would otherwise go to the host engine (qpd_decode_host below
+    qpd_info.host_max_frames), and a "GPU" parity case would test C++.  Decoders
+    read QPD_HOST_ENGINE when they are created.  Tests of the host engine itself
+    carry the host_engine marker and choose their engine explicitly."""
+    if request.node.get_closest_marker("gpu") is None or request.node.get_closest_marker("host_engine") is not None:
+        return
+    monkeypatch.setenv("QPD_HOST_ENGINE", "gpu")
 
 
 def golden_files(pattern="*.npz"):
@@ -71,15 +88,28 @@ def frame_lanes(info, frame):
     return frame // fpw_task, slot // per_set, (k * gs, (k + 1) * gs - 1)
 
 
-def assert_frames_equal(got, want, dec=None, label="", redecode=None, inputs=None):
+def assert_engine(dec, engine):
+    """The decoder's last decode call ran on `engine` ("gpu": the kernels; "host":
+    the host engine); None skips the check."""
+    if dec is None or engine is None:
+        return
+    ran = ENGINE_NAMES.get(int(dec.info()["last_engine"]), "?")
+    assert ran == engine, f"the last decode ran on the {ran} engine, this check is for the {engine} engine"
+
+
+def assert_frames_equal(got, want, dec=None, label="", redecode=None, inputs=None, engine="gpu"):
     """Bit-exact frame comparison that explains a mismatch instead of only
     counting it: for each differing frame (up to 8) the task / frame set /
     lanes it ran on, the differing bit positions and both bit strings; with
     `redecode(rows) -> bits` the differing frames are decoded again, alone, in
     a fresh decoder, which separates a deterministic difference (same result
     alone) from one that depended on the run.  Everything is also written as
-    JSON to $QPD_DIAG_DIR (default gpurun_out/), which gpurun copies back."""
+    JSON to $QPD_DIAG_DIR (default gpurun_out/), which gpurun copies back.
+    With `dec`, the decoder's last decode must have run on `engine` (default
+    the GPU kernels; None: no check)."""
     import json
+
+    assert_engine(dec, engine)
 
     got = np.asarray(got)
     want = np.asarray(want)

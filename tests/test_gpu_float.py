@@ -16,10 +16,14 @@ import os
 import numpy as np
 import pytest
 
-from conftest import golden_files, load_golden
+from conftest import assert_engine, golden_files, load_golden
 from test_float_oracle import CRC11, CRC24, FLOAT_KINDS, float_inputs, golden_quant, quant_for
 
 pytestmark = pytest.mark.gpu
+
+# Both engines behind the host-buffer calls, chosen explicitly (qpd_set_host_engine):
+# the kernels, and the host engine that serves per-frame calls (not the re-quantized kinds).
+ENGINES = ["gpu", pytest.param("host", marks=pytest.mark.host_engine)]
 
 
 @pytest.fixture(scope="module")
@@ -39,18 +43,23 @@ def _code(N, K):
     return mb, fm, C.identify_nodes(N, mb).astype(np.int32)
 
 
+@pytest.mark.parametrize("engine", ENGINES)
 @pytest.mark.parametrize("path", golden_files("float_*.npz"), ids=lambda p: os.path.basename(p)[:-4])
-def test_gpu_float_matches_golden(path, qpd):
+def test_gpu_float_matches_golden(path, engine, qpd):
     from quantized_decoder_polar_codes_amd.decoders import from_quant
 
     g = load_golden(path)
     kind = str(g["kind"])
+    if engine == "host" and kind.endswith(("Uniform", "Lloyd")):
+        pytest.skip("the host engine does not decode the re-quantized kinds (test_gpu_host_engine.py)")
     N, K, L = int(g["N"]), int(g["K"]), int(g["L"])
     kw = {}
     if kind == "CA-SCL":
         kw = dict(A=int(g["A"]), crc_n=int(g["crc_n"]), crc_loc=g["crc_loc"])
     dec = from_quant(kind, N, K, g["frozen"], L=L, node_type=g["node_type"], quant=golden_quant(g), **kw)
+    dec.set_host_engine("cpu" if engine == "host" else "gpu")
     got = dec.decode_batch(g["llr"])
+    assert_engine(dec, engine)
     assert got.shape == g["expected"].shape
     bad = np.flatnonzero((got != g["expected"]).any(1))
     assert bad.size == 0, f"{bad.size}/{len(got)} frames differ, first {bad[:5]}"
@@ -197,15 +206,22 @@ def test_gpu_lloyd_index_outside_reconstruction_is_reported(qpd):
     assert ok.shape == (4, K)
 
 
-def test_gpu_nan_path_metric_is_reported(qpd):
+@pytest.mark.parametrize("engine", ENGINES)
+def test_gpu_nan_path_metric_is_reported(engine, qpd):
     from quantized_decoder_polar_codes_amd.decoders import from_quant
 
+    mode = "cpu" if engine == "host" else "gpu"
     N, K = 64, 32
     mb, fm, nt = _code(N, K)
     llr = np.ones((2, N))
     llr[1, 0] = np.nan
     dec = from_quant("SCL", N, K, fm, L=4)
+    dec.set_host_engine(mode)
     with pytest.raises(ValueError, match="NaN"):
         dec.decode_batch(llr)
+    assert_engine(dec, engine)
+    assert dec.decode_batch(np.ones((2, N))).shape == (2, K)  # flag cleared
     sc = from_quant("SC", N, K, fm)  # SC has no sort: NaN flows through as in the reference
+    sc.set_host_engine(mode)
     assert sc.decode_batch(llr).shape == (2, K)
+    assert_engine(sc, engine)

@@ -15,7 +15,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import assert_frames_equal, golden_files, golden_packed, load_golden
+from conftest import assert_engine, assert_frames_equal, golden_files, golden_packed, load_golden
 
 pytestmark = pytest.mark.gpu
 
@@ -255,17 +255,20 @@ def test_torch_device_path_matches_host_path(qpd):
     assert (dev.cpu().numpy() == host).all()
 
 
-def test_out_of_range_symbol_is_reported(qpd):
+@pytest.mark.parametrize("engine", ["gpu", pytest.param("host", marks=pytest.mark.host_engine)])
+def test_out_of_range_symbol_is_reported(engine, qpd):
     from quantized_decoder_polar_codes_amd import lut as LU
 
     N, K = 64, 32
     p = LU.random_luts(N, 16, seed=1)
     fm, nt = _node_type(N, K)
     d = qpd.from_packed("SC-LUT", p, K, fm)
+    d.set_host_engine("cpu" if engine == "host" else "gpu")
     sym = np.zeros((3, N), dtype=np.int32)
     sym[1, 7] = 16
     with pytest.raises(ValueError):
         d.decode_batch(sym)
+    assert_engine(d, engine)
     d.decode_batch(np.zeros((3, N), dtype=np.int32))  # flag cleared
 
 
@@ -424,19 +427,24 @@ def test_kernel_timing_and_lds_probe(qpd):
     assert rates[_lib.QPD_PROBE_READ_B64] > rates[_lib.QPD_PROBE_BPERMUTE]
 
 
-def test_host_decode_reports_out_of_range_symbol(qpd):
-    """The per-frame host path (pinned staging, one stream sync) still raises on
-    a channel symbol outside [0, v) and recovers for the next call."""
+@pytest.mark.parametrize("engine", ["gpu", pytest.param("host", marks=pytest.mark.host_engine)])
+def test_host_decode_reports_out_of_range_symbol(engine, qpd):
+    """The per-frame host path (pinned staging, one stream sync; or the host
+    engine) still raises on a channel symbol outside [0, v) and recovers for
+    the next call."""
     from quantized_decoder_polar_codes_amd import lut as LU
 
     N, K = 128, 64
     fm, nt = _node_type(N, K)
     dec = qpd.from_packed("SCL-LUT", LU.minsum_uniform_luts(N), K, fm, L=4)
+    dec.set_host_engine("cpu" if engine == "host" else "gpu")
     good = np.random.default_rng(3).integers(0, 16, size=(5, N), dtype=np.int32)
     bad = good.copy()
     bad[2, 7] = 16
     with pytest.raises(ValueError, match="outside"):
         dec.decode_batch(bad)
+    assert_engine(dec, engine)
     a = dec.decode_batch(good)
     b = np.stack([dec.decode(x) for x in good])
+    assert_engine(dec, engine)
     assert np.array_equal(a, b)

@@ -111,3 +111,32 @@ def test_prefix_crc_aided(kind, qpd, monkeypatch):
     assert (a.info()["prefix_ops"] > 0) == (kind[3:] in SPLIT)
     ga = a.decode_batch(sym)
     assert np.array_equal(ga, b.decode_batch(sym))
+
+
+@pytest.mark.parametrize("scale", ["below", "above"])
+def test_prefix_guard_near_dbl_max_quanta(scale, qpd, oracle_mod):
+    """Leaf quanta near DBL_MAX: path metrics may overflow to +inf, where the
+    split's dead-slot seeding (path 0's rows) would differ from the reference's
+    copies of other dead paths.  Quanta up to DBL_MAX / 2N keep every metric
+    finite and take the split; larger ones decode unsplit.  Either way the bits
+    are the oracle's, on the kernels and on the host engine."""
+    from quantized_decoder_polar_codes_amd import lut as LU
+
+    N, K, L = 1024, 512, 8
+    n = 10
+    fm, nt = _code(N, K)
+    p = _tables(N, 4242)
+    vcl = p.vcl.copy()
+    bound = np.finfo(np.float64).max / (2 * N)
+    top = np.abs(vcl[n - 1]).max()
+    vcl[n - 1] *= (0.999 * bound if scale == "below" else 64 * bound) / top
+    assert np.isfinite(vcl).all()
+    q = LU.PackedLUT(N=p.N, v=p.v, lut_f=p.lut_f, f_base=p.f_base, f_step=p.f_step, lut_g=p.lut_g, g_base=p.g_base,
+                     g_step=p.g_step, vcl=np.ascontiguousarray(vcl))
+    sym = np.random.default_rng(8).integers(0, 16, size=(48, N), dtype=np.int32)
+    dec = qpd.from_packed("SCL-LUT", q, K, fm, L=L)
+    assert (dec.info()["prefix_ops"] > 0) == (scale == "below")
+    want = oracle_mod.decode_lut("SCL-LUT", q, K, L, fm, sym)
+    assert_frames_equal(dec.decode_batch(sym), want, dec, f"prefix-dblmax-{scale}")
+    dec.set_host_engine("cpu")
+    assert_frames_equal(dec.decode_batch(sym), want, dec, f"prefix-dblmax-{scale}-host", engine="host")
