@@ -79,6 +79,7 @@ struct qpd_decoder {
     int sets = 1;  // fast engine: frame sets per wave (lut_fast_kernel NS)
     bool l8 = false;  // fast engine: list decoder with L = 8 (select_survivors8)
     bool r1l = false;  // fast engine: an R1 node needs r1_large (the R1L instantiation)
+    bool pw1 = false;  // fast engine: one pointer word per path (compact_pointer_fields)
     bool pre = false;         // fast engine pre-mode: root_pre_kernel, then the decode on its rows
     int64_t pre_chunk = 0;    // frames per pre-pass chunk
     int64_t pre_cap = 0;      // frames pre_buf holds
@@ -791,9 +792,16 @@ int ensure_records(DeviceBuf &b, size_t &cap, int64_t Bc, int rec, int paths) {
 #endif
 constexpr int kDefaultSets = QPD_DEFAULT_SETS;
 
-// Instantiations of lut_fast_kernel<KIND, NS, L8, R1L>.
-const void *fast_kernel(int kind, int sets, bool l8, bool r1l) {
+// Instantiations of lut_fast_kernel<KIND, NS, L8, R1L, PFX, PW1>; pw1: the
+// op list's pointer fields fit one word (compact_pointer_fields; SCL-LUT only).
+const void *fast_kernel(int kind, int sets, bool l8, bool r1l, bool pw1) {
     using namespace qpd;
+    if (kind == QPD_SCL_LUT && pw1) {
+        if (sets == 2) return l8 ? reinterpret_cast<const void *>(&lut_fast_kernel<K_SCL_LUT, 2, true, false, false, true>)
+                                 : reinterpret_cast<const void *>(&lut_fast_kernel<K_SCL_LUT, 2, false, false, false, true>);
+        return l8 ? reinterpret_cast<const void *>(&lut_fast_kernel<K_SCL_LUT, 1, true, false, false, true>)
+                  : reinterpret_cast<const void *>(&lut_fast_kernel<K_SCL_LUT, 1, false, false, false, true>);
+    }
 #define QPD_FK(K, S, E) reinterpret_cast<const void *>(&lut_fast_kernel<K, S, E>)
 #define QPD_FKR(S, E) reinterpret_cast<const void *>(&lut_fast_kernel<K_FASTSCL_LUT, S, E, true>)
     switch (kind) {
@@ -822,14 +830,88 @@ const void *fast_kernel(int kind, int sets, bool l8, bool r1l) {
 #undef QPD_FK
 }
 
-const void *prefix_kernel(int kind, int sets) {
+const void *prefix_kernel(int kind, int sets, bool pw1) {
     using namespace qpd;
     switch (kind) {
         case QPD_SCL_LUT:
-            return sets == 2 ? reinterpret_cast<const void *>(&lut_prefix_kernel(K_SCL_LUT, 2))
-                             : reinterpret_cast<const void *>(&lut_prefix_kernel(K_SCL_LUT, 1));
+            if (pw1)
+                return sets == 2 ? reinterpret_cast<const void *>(&lut_prefix_kernel(K_SCL_LUT, 2, true))
+                                 : reinterpret_cast<const void *>(&lut_prefix_kernel(K_SCL_LUT, 1, true));
+            return sets == 2 ? reinterpret_cast<const void *>(&lut_prefix_kernel(K_SCL_LUT, 2, false))
+                             : reinterpret_cast<const void *>(&lut_prefix_kernel(K_SCL_LUT, 1, false));
         default: return nullptr;
     }
+}
+
+// One pointer word per path (PathT<true>, qpd_fast.hip): the S-row and U-row
+// pointer fields the op lists read or set, by op type (the access pattern of
+// each op's code), packed into consecutive 4-bit positions of one word.
+// False (lists unchanged) when they need more than 16 fields.
+bool compact_pointer_fields(const std::vector<std::vector<qpd::MOp> *> &lists) {
+    using namespace qpd;
+    int pos[2][kMaxDepth + 1];
+    for (auto &a : pos)
+        for (int &x : a) x = -1;
+    auto each = [&](qpd::MOp &m, auto &&fn) {  // fn(slot 0 = S / 1 = U, int &sh)
+        const int fl = m.flags;
+        const bool src_row = !(fl & (MF_CHAN | MF_PRE));
+        switch (m.type) {
+            case OP_F:
+            case OP_G:
+                if (src_row) fn(0, m.sh_src);
+                if (m.type == OP_G) fn(1, m.sh_u);  // (MF_GSEL reads U[1] through it too)
+                fn(0, m.sh_dst);
+                break;
+            case OP_LEAF_L:
+            case OP_LEAF_R:
+                if (src_row) fn(0, m.sh_src);
+                if (m.type == OP_LEAF_R) fn(1, m.sh_u);
+                else fn(1, m.sh_dst);
+                break;
+            case OP_COMB:
+                fn(1, m.sh_u);
+                if (!(fl & MF_TO_R)) fn(1, m.sh_dst);
+                break;
+            case OP_BOT3:
+                if (src_row) fn(0, m.sh_src);
+                if (fl & (MF_BG | MF_BCOMB)) fn(1, m.sh_u);
+                if (!(fl & MF_TO_R)) fn(1, m.sh_dst);
+                break;
+            case OP_IMPORT: break;
+            case OP_EXPORT:
+                if (fl & MF_VIA_PS) fn(0, m.sh_src);
+                if (fl & MF_VIA_PU) fn(1, m.sh_src);
+                break;
+            default:  // special nodes
+                fn(0, m.sh_src);
+                if (!(fl & MF_TO_R)) fn(1, m.sh_dst);
+                break;
+        }
+    };
+    int used = 0;
+    for (auto *l : lists)
+        for (qpd::MOp &m : *l)
+            each(m, [&](int sl, int &sh) {
+                int &p = pos[sl][sh / 4];
+                if (p < 0) p = used++;
+            });
+    if (used > 16) return false;
+    for (auto *l : lists)
+        for (qpd::MOp &m : *l) {
+            // every field of an op is rewritten once (fields shared by two
+            // roles, e.g. sh_src of a special node, are read before any write)
+            int sh_src = m.sh_src, sh_u = m.sh_u, sh_dst = m.sh_dst;
+            each(m, [&](int sl, int &sh) {
+                const int np = 4 * pos[sl][sh / 4];
+                if (&sh == &m.sh_src) sh_src = np;
+                else if (&sh == &m.sh_u) sh_u = np;
+                else sh_dst = np;
+            });
+            m.sh_src = sh_src;
+            m.sh_u = sh_u;
+            m.sh_dst = sh_dst;
+        }
+    return true;
 }
 
 // Task queue of the persistent kernels: one counter, never reset (wave_take).
@@ -1004,6 +1086,7 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     place_syncs(pp.st1, true);
     place_syncs(pp.st2, true);
     place_syncs(mops, c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT);
+    if (c->kind == QPD_SCL_LUT && !getenv("QPD_NO_PW1")) d->pw1 = compact_pointer_fields({&mops, &pp.st1, &pp.st2});
     d->pfx_nops = (int)pp.st1.size();
     d->pfx_sets = std::min(d->sets, 2);
     // prefix_kernel() instantiates NS = 1 and 2 only: fast_launch's task count
@@ -1058,7 +1141,8 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         const hipError_t oe =
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fast_kernel(d->kind, d->sets, d->l8, d->r1l), 64, d->lds_bytes);
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fast_kernel(d->kind, d->sets, d->l8, d->r1l, d->pw1), 64,
+                                                         d->lds_bytes);
         if (oe != hipSuccess || per_cu <= 0) per_cu = 16;
         mw = std::max(1, ncu) * per_cu;
     }
@@ -1442,7 +1526,7 @@ int fast_launch(qpd_decoder *d, qpd::FastPlan fp, const int32_t *in, int64_t Bc,
                 bool prefix = false) {
     const int sets = prefix ? d->pfx_sets : d->sets;
     const int64_t tw = (int64_t)fp.fpw * sets;  // frames per wave task
-    const void *kfn = prefix ? prefix_kernel(d->kind, sets) : fast_kernel(d->kind, d->sets, d->l8, d->r1l);
+    const void *kfn = prefix ? prefix_kernel(d->kind, sets, d->pw1) : fast_kernel(d->kind, d->sets, d->l8, d->r1l, d->pw1);
     if (!kfn) return fail(QPD_E_INVALID, "bad kind");
     const int64_t fgroups = (Bc + tw - 1) / tw;
     int fgrid = (int)std::min<int64_t>(fgroups, d->max_waves);

@@ -165,9 +165,10 @@ __device__ __forceinline__ Sel select_survivors(double kk, double kf, int gl, in
 }
 
 // L = 8 (lane groups of 8): ranks from the 7 DPP partners, branch-free
-// scatter (ranks >= 8 go to a per-lane junk slot), so several independent
-// selections can interleave in one basic block.  `sel` = 128 ints.
-__device__ __forceinline__ Sel select_survivors8(double kk, double kf, int gl, int gbase, int lane, int *sel) {
+// scatter (ranks >= 8 go to a per-lane junk slot at sel[junk + lane]), so
+// several independent selections can interleave in one basic block.
+__device__ __forceinline__ Sel select_survivors8(double kk, double kf, int gl, int gbase, int lane, int *sel,
+                                                 int junk = 64) {
     const uint64_t K = __builtin_bit_cast(uint64_t, kk), F = __builtin_bit_cast(uint64_t, kf);
     const uint64_t hk = dpp64<kDppHalfMirror>(K), hf = dpp64<kDppHalfMirror>(F);
     const uint64_t F1 = F + 1;
@@ -179,8 +180,8 @@ __device__ __forceinline__ Sel select_survivors8(double kk, double kf, int gl, i
     rank8_partner<5>(K, F, F1, hk, hf, gl, rk, rf);
     rank8_partner<6>(K, F, F1, hk, hf, gl, rk, rf);
     rank8_partner<7>(K, F, F1, hk, hf, gl, rk, rf);
-    sel[rk < 8 ? gbase + rk : 64 + lane] = gl;
-    sel[rf < 8 ? gbase + rf : 64 + lane] = gl + 8;
+    sel[rk < 8 ? gbase + rk : junk + lane] = gl;
+    sel[rf < 8 ? gbase + rf : junk + lane] = gl + 8;
     lds_order();
     const int c = sel[gbase + gl];
     lds_order();

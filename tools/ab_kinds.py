@@ -14,7 +14,7 @@ import bench  # noqa: E402
 kinds = sys.argv[1:] or ["SCL-LUT", "FastSCL-LUT"]
 F = int(os.environ.get("AB_FRAMES", "1048576"))
 for kind in kinds:
-    wl = bench.workload(1024, 512, 8, kind, F, 2.0)
+    wl = bench.workload(1024, 512, 8, kind, F, 2.0, max_waves=int(os.environ.get("QPD_MAX_WAVES", "0")))
     d, sym = wl.dec, wl.sym
     out = d.decode_batch(sym)
     torch.cuda.synchronize()
