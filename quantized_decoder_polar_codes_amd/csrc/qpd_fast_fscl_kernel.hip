@@ -1,4 +1,20 @@
-// qpd_fast.hip -- the fast gfx950 LUT decode kernel (one table per node, v <= 16).
+// qpd_fast_fscl_kernel.hip -- the decode kernel templates the FastSCL-LUT unit
+// (qpd_fast_fscl.hip) instantiates: the round-3 state of qpd_fast.hip, in its
+// own namespace (qpd::fscl).
+//
+// Why a separate copy: the FastSCL-LUT kernel runs one frame set per wave at 6
+// waves per SIMD (80 VGPRs) and spills around 160 B per lane, and where its
+// register allocator puts those spills decides its speed.  Round 4 changed the
+// shared kernel for SCL-LUT (set-interleaved rows, one pointer word, staged BOT3
+// loads, the identity test's ballot masks, fork flags) -- for FastSCL-LUT every
+// one of those is the same computation, yet compiled with them it ran at
+// 24.2 M frames/s instead of 31.8 M (profiles/r04i_ab.txt, profiles/r04j_ab.txt:
+// the same bits; reverting single changes recovered part of it, this copy all of
+// it).  The host plan is the same for both (FastPlan, MOp, one set: the same
+// row, slab and selection layout; two pointer words), so the FastSCL-LUT unit
+// compiles this frozen copy and the SCL-LUT kernel moves on without it.  Changes
+// to the FastSCL-LUT kernel go here; parity: tests/test_gpu_*.py (FastSCL cases).
+// (round-3 header of qpd_fast.hip:) the fast gfx950 LUT decode kernel (one table per node, v <= 16).
 //
 // Same algorithm, traversal and list management as the generic kernel
 // (qpd_generic.hip: one lane per list path, G = pow2 >= L lanes per frame,
@@ -29,6 +45,7 @@
 #include "stl_sort.hpp"
 
 namespace qpd {
+namespace fscl {
 
 constexpr int OP_BOT3 = 9;    // fused bottom subtree of height 3 (fast engine only)
 constexpr int OP_IMPORT = 10; // frozen-prefix stages (see lut_prefix_kernel): rows / metric from a stage's records, or zeros
@@ -126,39 +143,31 @@ struct FastPlan {
 // reached through a buffer descriptor (32-bit lane offsets; distinct
 // instructions, so the compiler never folds the two spaces into one flat
 // access that would wait on both counters).
-// A wave's `ns` frame sets interleave their rows, in LDS and in the slab: row r
-// of set s is the wave's row r * ns + s.  The sets share one LDS base and one
-// slab descriptor and a set's view differs only by s rows -- an immediate
-// offset in its LDS / buffer instructions (`so` bytes, constant after the set
-// loops unroll) instead of a base register and a descriptor per set.
 struct Mem {
-    uint32_t *lds;              // this set's LDS row 0 (the wave's base + s rows)
-    uint32_t *gp;               // this set's slab row 0 (R1 argsort arrays)
-    __amdgpu_buffer_rsrc_t rs;  // the wave's slab, all sets
-    int so;                     // this set's byte offset in a slab row group (s * 256)
-    int ns;                     // frame sets of the wave: the row stride in rows
-    __device__ __forceinline__ int rw(int row) const { return row * ns * 64; }  // words to row `row`
+    uint32_t *lds;
+    uint32_t *gp;               // slab base (R1 argsort arrays)
+    __amdgpu_buffer_rsrc_t rs;  // the same slab as a buffer resource
     // `row` wave-uniform: it rides in the buffer op's SGPR offset
     __device__ __forceinline__ uint32_t ld(bool in_lds, int row, int lane) const {
-        if (in_lds) return lds[rw(row) + lane];
-        return __builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, row * ns * 256 + so, QPD_SLAB_AUX);
+        if (in_lds) return lds[row * 64 + lane];
+        return __builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, row * 256, QPD_SLAB_AUX);
     }
     __device__ __forceinline__ void st(bool in_lds, int row, int lane, uint32_t v) const {
         if (in_lds)
-            lds[rw(row) + lane] = v;
+            lds[row * 64 + lane] = v;
         else
-            __builtin_amdgcn_raw_buffer_store_b32(v, rs, lane * 4, row * ns * 256 + so, QPD_SLAB_AUX);
+            __builtin_amdgcn_raw_buffer_store_b32(v, rs, lane * 4, row * 256, QPD_SLAB_AUX);
     }
     // any row (per-lane)
     __device__ __forceinline__ uint32_t ldv(bool in_lds, int row, int lane) const {
-        if (in_lds) return lds[rw(row) + lane];
-        return __builtin_amdgcn_raw_buffer_load_b32(rs, (rw(row) + lane) * 4 + so, 0, QPD_SLAB_AUX);
+        if (in_lds) return lds[row * 64 + lane];
+        return __builtin_amdgcn_raw_buffer_load_b32(rs, (row * 64 + lane) * 4, 0, QPD_SLAB_AUX);
     }
     __device__ __forceinline__ void stv(bool in_lds, int row, int lane, uint32_t v) const {
         if (in_lds)
-            lds[rw(row) + lane] = v;
+            lds[row * 64 + lane] = v;
         else
-            __builtin_amdgcn_raw_buffer_store_b32(v, rs, (rw(row) + lane) * 4 + so, 0, QPD_SLAB_AUX);
+            __builtin_amdgcn_raw_buffer_store_b32(v, rs, (row * 64 + lane) * 4, 0, QPD_SLAB_AUX);
     }
 };
 
@@ -417,17 +426,13 @@ __device__ __forceinline__ void gsel_op(const Mem (&M)[NS], const MOp &op, const
     }
 }
 
-// Per-lane argsort arrays (global scratch) for the R1 node; rows of this set
-// (stride `rs` words, see Mem), a key's double as two rows (low, high word).
+// Per-lane argsort arrays (global scratch) for the R1 node.
 struct FastSortSeq {
     uint32_t *glb;
-    int io, ko, lane, rs;
-    __device__ int get(int p) { return (int)glb[(size_t)(io + p) * rs + lane]; }
-    __device__ void set(int p, int e) { glb[(size_t)(io + p) * rs + lane] = (uint32_t)e; }
-    __device__ double key(int e) {
-        const uint64_t lo = glb[(size_t)(ko + 2 * e) * rs + lane], hi = glb[(size_t)(ko + 2 * e + 1) * rs + lane];
-        return __builtin_bit_cast(double, lo | (hi << 32));
-    }
+    int io, ko, lane;
+    __device__ int get(int p) { return (int)glb[(size_t)(io + p) * 64 + lane]; }
+    __device__ void set(int p, int e) { glb[(size_t)(io + p) * 64 + lane] = (uint32_t)e; }
+    __device__ double key(int e) { return ((double *)(glb + (size_t)(ko + 2 * e) * 64))[lane]; }
     __device__ bool less(int a, int b) { return key(a) < key(b); }
 };
 
@@ -457,43 +462,18 @@ __device__ __forceinline__ Pre fetch_pre(const FastPlan &P, const MOp &op, int l
 // ---------------------------------------------------------------------------
 // List state and the fork (mink, SCLLUTDecoder.cpp:105-144).
 //
-// The speculative right-leaf lookup (bot_pair): +1.3 % at 4 waves per SIMD,
-// -1 % at the 5 the SCL-LUT kernel runs now (its registers; r04g / r04j): off.
-#ifndef QPD_SPEC_RIGHT
-#define QPD_SPEC_RIGHT 0
-#endif
 // A wave runs NS independent frame sets through the same op stream.  The op
 // records, the per-node tables and all scalar control are shared; the sets'
 // dependency chains (LDS lookups, survivor selection, fork shuffles) are
 // independent and interleave, which hides the LDS latency that bounds a
 // single set.
 // ---------------------------------------------------------------------------
-// A path's metric and slot pointers: ps holds the S-row pointer fields, pu
-// the U-row ones.  PW1: the host packed every field the op list uses into one
-// word (at most 16 of them: SCL-LUT up to N = 2048, qpd_capi.hip:
-// compact_pointer_fields), so U() is the same word -- two registers and two
-// shuffles per fork less per frame set.
-template <bool PW1>
-struct PathT;
-template <>
-struct PathT<false> {
+struct Path {
     double pm;
     uint64_t ps, pu;
-    __device__ __forceinline__ uint64_t &U() { return pu; }
-    __device__ __forceinline__ void move(int p) {  // take lane p's pointers (a fork)
-        ps = shfl64(ps, p);
-        pu = shfl64(pu, p);
-    }
-};
-template <>
-struct PathT<true> {
-    double pm;
-    uint64_t ps;
-    __device__ __forceinline__ uint64_t &U() { return ps; }
-    __device__ __forceinline__ void move(int p) { ps = shfl64(ps, p); }
 };
 
-constexpr int kSelInts = 128;  // per set: 64 slots + 64 junk slots (select_survivors8): two rows after the set's
+constexpr int kSelInts = 128;  // per set: 64 slots + 64 junk slots (select_survivors8)
 
 // max of two non-negative doubles given as bits (one v_max_f64).
 __device__ __forceinline__ uint64_t dmax_bits(uint64_t a, uint64_t b) {
@@ -511,77 +491,42 @@ __device__ __forceinline__ uint64_t dmax_bits(uint64_t a, uint64_t b) {
 // ERR_NAN_PM in the generic engine; LUT quanta are finite): max over doubles =
 // max over their bits.  v_max_f64 by inline asm: the builtin would
 // canonicalize the DPP operands first (two more VALU per step).
-//
-// First a conservative test on the high words alone (sign, exponent and the
-// top 20 mantissa bits; keys are >= +0, so a larger high word is a larger
-// double): strictly increasing keeps and every flip strictly above the
-// largest keep's high word imply the identity.  32-bit words take the DPP
-// lane moves inside the max / compare instructions (one VALU per step instead
-// of two moves and a v_max_f64); only when it cannot decide (equal high words:
-// near-ties) does the exact 64-bit test run.
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, true);
-}
-
 __device__ __forceinline__ bool keep_all8(uint64_t K, uint64_t F, int gl) {
-#if defined(QPD_EXP_IDENT)  // timing experiments only (wrong results): every selection the identity / none
-    return QPD_EXP_IDENT;
-#endif
-#ifdef QPD_HI_IDENT  // measured -0.5 % on SCL-LUT (r04e): off
-    {
-        const uint32_t kh = (uint32_t)(K >> 32), fh = (uint32_t)(F >> 32);
-        uint32_t m = kh;
-        m = max(m, dpp32<kDppXor1>(m));
-        m = max(m, dpp32<kDppXor2>(m));
-        m = max(m, dpp32<kDppHalfMirror>(m));
-        const uint32_t khn = dpp32<kDppRowShl1>(kh);
-        // lanes with gl == 7 (every 8th) have no next slot: their sortedness bit is set
-        const uint64_t up = __builtin_amdgcn_ballot_w64(fh > m);
-        const uint64_t srt = __builtin_amdgcn_ballot_w64(khn > kh) | 0x8080808080808080ull;
-        if ((up & srt) == ~0ull) return true;
-    }
-#endif
     uint64_t mk = K;
     mk = dmax_bits(mk, dpp64<kDppXor1>(mk));
     mk = dmax_bits(mk, dpp64<kDppXor2>(mk));
     mk = dmax_bits(mk, dpp64<kDppHalfMirror>(mk));  // lane i^7 lies in the other quad
     const uint64_t Kn = dpp64<kDppRowShl1>(K);       // keep of slot gl+1
-    (void)gl;
-    return (__builtin_amdgcn_ballot_w64(F >= mk) & (__builtin_amdgcn_ballot_w64(K <= Kn) | 0x8080808080808080ull)) == ~0ull;
+    return __ballot(F >= mk && (gl == 7 || K <= Kn)) == ~0ull;
 }
 
 // Info leaf with quanta dm: keep the L best of {keep, flip} candidates.
 // Returns the new decision; `extra` words follow the surviving lineage.
-// `moved` (wave-uniform): the selection was not the identity (paths moved).
-template <bool L8, int NX, class Path>
-__device__ __forceinline__ uint32_t leaf_fork(Path &st, double dm, int gl, int gbase, int L, int lane, int *sel, int sj,
-                                              uint32_t (&extra)[NX], bool &moved) {
+template <bool L8, int NX>
+__device__ __forceinline__ uint32_t leaf_fork(Path &st, double dm, int gl, int gbase, int L, int lane, int *sel,
+                                              uint32_t (&extra)[NX]) {
     const double kf = st.pm + fabs(dm);
     const uint32_t hd = dm < 0;  // H4: SCL family `< 0`
     // Fast path (about 2/3 of the info leaves on the bench channel): the
     // selection is the identity, the decision the hard one.
-    moved = false;
     if constexpr (L8)
         if (keep_all8(__builtin_bit_cast(uint64_t, st.pm), __builtin_bit_cast(uint64_t, kf), gl)) return hd;
-    moved = true;
-    const Sel sl = L8 ? select_survivors8(st.pm, kf, gl, gbase, lane, sel, sj) : select_survivors(st.pm, kf, gl, gbase, L, sel);
+    const Sel sl = L8 ? select_survivors8(st.pm, kf, gl, gbase, lane, sel) : select_survivors(st.pm, kf, gl, gbase, L, sel);
     const int p = gbase + sl.parent;
     const uint32_t dec = (uint32_t)lane_read((int)hd, p) ^ (sl.upper ? 1u : 0u);
     st.pm = pick(sl.upper, shfld(kf, p), shfld(st.pm, p));
-    st.move(p);
+    st.ps = shfl64(st.ps, p);
+    st.pu = shfl64(st.pu, p);
 #pragma unroll
     for (int i = 0; i < NX; ++i) extra[i] = (uint32_t)lane_read((int)extra[i], p);
     return dec;
 }
 
 // One leaf decision for every set.  `frozen` is wave-uniform.
-template <bool kList, bool L8, int NS, int NX, class Path>
+template <bool kList, bool L8, int NS, int NX>
 __device__ __forceinline__ void leaf_decide(Path (&st)[NS], const double (&dm)[NS], bool frozen, int gl, int gbase,
                                             int L, int lane, int *sel, int sstride, uint32_t (&extra)[NS][NX],
-                                            uint32_t (&dec)[NS], bool (&moved)[NS]) {
-#pragma unroll
-    for (int s = 0; s < NS; ++s) moved[s] = false;
+                                            uint32_t (&dec)[NS]) {
     if (!kList) {
 #pragma unroll
         for (int s = 0; s < NS; ++s) dec[s] = frozen ? 0u : (uint32_t)(dm[s] <= 0);  // H4: SC family `<= 0`
@@ -598,8 +543,7 @@ __device__ __forceinline__ void leaf_decide(Path (&st)[NS], const double (&dm)[N
         return;
     }
 #pragma unroll
-    for (int s = 0; s < NS; ++s)
-        dec[s] = leaf_fork<L8>(st[s], dm[s], gl, gbase, L, lane, sel + sstride * s, NS * sstride, extra[s], moved[s]);
+    for (int s = 0; s < NS; ++s) dec[s] = leaf_fork<L8>(st[s], dm[s], gl, gbase, L, lane, sel + sstride * s, extra[s]);
 }
 
 // ---------------------------------------------------------------------------
@@ -618,50 +562,26 @@ __device__ __forceinline__ uint32_t g_pair(uint32_t T, uint32_t c2, uint32_t w2)
     return lut_vec<2>(T, w2, w2 >> 8, c2);
 }
 
-template <bool kList, bool L8, bool SPEC, int NS, class Path>
+template <bool kList, bool L8, int NS>
 __device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], uint32_t Tf, int fo, uint32_t Tg,
                                          double V, int vo, int fr, int gl, int gbase, int L, int lane, int *sel, int sstride,
                                          uint32_t (&c)[NS]) {
     double dm[NS];
     uint32_t bl[NS], br[NS];
-    bool moved[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const uint32_t a = (x[s][1] >> 16) & 15u, b = (x[s][1] >> 20) & 15u;
         dm[s] = 0;
         if (kList || !(fr & 1)) dm[s] = shfld(V, vo + (int)lut4(Tf, ((a << 4) | b) + fo));
     }
-#if QPD_SPEC_RIGHT  // (SPEC: SCL-LUT; the FastSCL unit measured slower with it)
-    // The right leaf's quanta for the decision the left leaf takes when its
-    // selection is the identity (its hard decision, or 0 if frozen), looked up
-    // before the left fork's test resolves: the lookup latency leaves the
-    // chain of the ~2/3 of forks that move nothing; a fork that moves paths
-    // looks it up again from the surviving lineage's word.
-    double sdm[NS];
-    if constexpr (kList && L8 && SPEC) {
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            const uint32_t a = (x[s][1] >> 16) & 15u, b = (x[s][1] >> 20) & 15u;
-            const uint32_t hb = (fr & 1) ? 0u : (uint32_t)(dm[s] < 0);  // H4: SCL family `< 0`
-            sdm[s] = shfld(V, vo + 16 + (int)lut4(Tg, (hb << 8) | (a << 4) | b));
-        }
-    }
-#endif
-    leaf_decide<kList, L8>(st, dm, fr & 1, gl, gbase, L, lane, sel, sstride, x, bl, moved);
+    leaf_decide<kList, L8>(st, dm, fr & 1, gl, gbase, L, lane, sel, sstride, x, bl);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         x[s][1] = (x[s][1] & ~(1u << 24)) | (bl[s] << 24);
         const uint32_t a = (x[s][1] >> 16) & 15u, b = (x[s][1] >> 20) & 15u;
-#if QPD_SPEC_RIGHT
-        if constexpr (kList && L8 && SPEC) {
-            dm[s] = sdm[s];
-            if (moved[s]) dm[s] = shfld(V, vo + 16 + (int)lut4(Tg, (bl[s] << 8) | (a << 4) | b));
-            continue;
-        }
-#endif
         if (kList || !(fr & 2)) dm[s] = shfld(V, vo + 16 + (int)lut4(Tg, (bl[s] << 8) | (a << 4) | b));
     }
-    leaf_decide<kList, L8>(st, dm, fr & 2, gl, gbase, L, lane, sel, sstride, x, br, moved);
+    leaf_decide<kList, L8>(st, dm, fr & 2, gl, gbase, L, lane, sel, sstride, x, br);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const uint32_t bl2 = (x[s][1] >> 24) & 1u;
@@ -669,47 +589,29 @@ __device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], u
     }
 }
 
-// The subtree runs in four stages -- A: q0 left + leaves 0, 1; B: q1 g +
-// leaves 2, 3; C: q0 right + leaves 4, 5; D: q2 g + leaves 6, 7 -- and each
-// stage issues the table / quanta loads of the next one (LAZY: SCL-LUT, with
-// QPD_BOT3_LAZY; +0.5 % there at 5 waves, r04h), so at most about
-// 11 of them are live at once: the register budget of a fifth wave per SIMD.
-// `prefetch_next` issues the next op's operand prefetch at the start of stage
-// D instead of at the start of this op (4 registers less through stages A-C).
-#ifndef QPD_BOT3_LAZY
-#define QPD_BOT3_LAZY 1
-#endif
-template <bool kList, bool L8, bool LAZY, int NS, class PF, class Path>
+template <bool kList, bool L8, int NS>
 __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], const MOp &op,
                                         const int32_t *const (&y)[NS], Path (&st)[NS], uint32_t Tf0, uint32_t T2, int gl,
-                                        int gbase, int L, int *sel, int sstride, int lane, PF &&prefetch_next) {
+                                        int gbase, int L, int *sel, int sstride, int lane) {
     const int p0 = op.tab * QPD_EXP_TABMUL;
     const int fr = op.cnt;
     const uint32_t *ft = P.f_tab, *gt = P.g_tab;
     // Tables of the 7 internal nodes (q0's f table arrives prefetched).  Two
     // 32-dword f tables share one register (lanes 0-31 | 32-63: p and p+1 are
     // adjacent), addressed by adding 256 to the nibble index of the second.
+    const uint32_t Tg0 = tab_ld(gt, p0 * 64, lane);
     const int p1 = 2 * p0 + 1, p3 = 4 * p0 + 3;
+    const uint32_t Tf12 = tab_ld(ft, p1 * 32, lane), Tg1 = tab_ld(gt, p1 * 64, lane), Tg2 = tab_ld(gt, (p1 + 1) * 64, lane);
+    const uint32_t Tf34 = tab_ld(ft, p3 * 32, lane), Tg3 = tab_ld(gt, p3 * 64, lane), Tg4 = tab_ld(gt, (p3 + 1) * 64, lane);
+    const uint32_t Tf56 = tab_ld(ft, (p3 + 2) * 32, lane), Tg5 = tab_ld(gt, (p3 + 2) * 64, lane),
+                   Tg6 = tab_ld(gt, (p3 + 3) * 64, lane);
     // Leaf quanta vcl[n-1][8*node + j][s] of the 8 leaves, four leaves per
     // register: lane 16*jj + s holds leaf 4*h + jj (v <= 16).
     const int v = P.v;
     const int s16 = lane & 15, j16 = lane >> 4;
     const double *vb = P.vcl + op.vrow * QPD_EXP_TABMUL;
-    // stage A's operands, and B's
-    const uint32_t Tf12 = tab_ld(ft, p1 * 32, lane);
-    const uint32_t Tf34 = tab_ld(ft, p3 * 32, lane), Tg3 = tab_ld(gt, p3 * 64, lane);
     const double Vlo = s16 < v ? vb[j16 * v + s16] : 0.0;
-    const uint32_t Tg1 = tab_ld(gt, p1 * 64, lane), Tg4 = tab_ld(gt, (p3 + 1) * 64, lane);
-    uint32_t Tg0 = 0, Tf56 = 0, Tg5 = 0, Tg2 = 0, Tg6 = 0;
-    double Vhi = 0.0;
-    if constexpr (!LAZY) {
-        Tg0 = tab_ld(gt, p0 * 64, lane);
-        Tf56 = tab_ld(ft, (p3 + 2) * 32, lane);
-        Tg5 = tab_ld(gt, (p3 + 2) * 64, lane);
-        Tg2 = tab_ld(gt, (p1 + 1) * 64, lane);
-        Tg6 = tab_ld(gt, (p3 + 3) * 64, lane);
-        Vhi = s16 < v ? vb[(4 + j16) * v + s16] : 0.0;
-    }
+    const double Vhi = s16 < v ? vb[(4 + j16) * v + s16] : 0.0;
     uint32_t x[NS][2], c[NS];
     if (op.flags & MF_BFG) {
         // The depth n-4 parent's f / g (SCLLUTDecoder.cpp:83-89 / :157-164,
@@ -719,7 +621,7 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
         for (int s = 0; s < NS; ++s) {
             const int src = gbase + pfield(st[s].ps, op.sh_src);
             const uint32_t a = M[s].ld(sl, op.src_row, src), b = M[s].ld(sl, op.src_row + 1, src);
-            const uint32_t ub = (op.flags & MF_BG) ? M[s].ld(ul, op.u_row, gbase + pfield(st[s].U(), op.sh_u)) : 0u;
+            const uint32_t ub = (op.flags & MF_BG) ? M[s].ld(ul, op.u_row, gbase + pfield(st[s].pu, op.sh_u)) : 0u;
             x[s][0] = lut_vec<8>(T2, a, b, ub);
         }
     } else {
@@ -732,23 +634,13 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
         const uint32_t w2 = lut_vec<4>(Tf0, x[s][0], x[s][0] >> 16, 0u);
         x[s][1] = w2 | (f_pair(Tf12, 0u, w2) << 16);
     }
-    bot_pair<kList, L8, LAZY>(st, x, Tf34, 0, Tg3, Vlo, 0, fr, gl, gbase, L, lane, sel, sstride, c);  // leaves 0, 1
-    if constexpr (LAZY) {  // stage C's operands
-        Tg0 = tab_ld(gt, p0 * 64, lane);
-        Tf56 = tab_ld(ft, (p3 + 2) * 32, lane);
-        Tg5 = tab_ld(gt, (p3 + 2) * 64, lane);
-        Vhi = s16 < v ? vb[(4 + j16) * v + s16] : 0.0;
-    }
+    bot_pair<kList, L8>(st, x, Tf34, 0, Tg3, Vlo, 0, fr, gl, gbase, L, lane, sel, sstride, c);  // leaves 0, 1
 #pragma unroll
     for (int s = 0; s < NS; ++s) {  // q1: W1 = g(W2, c2)
         x[s][1] = (x[s][1] & ~(3u << 25)) | (c[s] << 25);
         x[s][1] = (x[s][1] & ~(0xffu << 16)) | (g_pair(Tg1, c[s], x[s][1] & 0xffffu) << 16);
     }
-    bot_pair<kList, L8, LAZY>(st, x, Tf34, 256, Tg4, Vlo, 32, fr >> 2, gl, gbase, L, lane, sel, sstride, c);  // leaves 2, 3
-    if constexpr (LAZY) {  // stage D's operands
-        Tg2 = tab_ld(gt, (p1 + 1) * 64, lane);
-        Tg6 = tab_ld(gt, (p3 + 3) * 64, lane);
-    }
+    bot_pair<kList, L8>(st, x, Tf34, 256, Tg4, Vlo, 32, fr >> 2, gl, gbase, L, lane, sel, sstride, c);  // leaves 2, 3
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const uint32_t c2 = (x[s][1] >> 25) & 3u;
@@ -757,14 +649,13 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
         const uint32_t w2 = lut_vec<4>(Tg0, x[s][0], x[s][0] >> 16, c3);
         x[s][1] = w2 | (f_pair(Tf12, 3u, w2) << 16) | (c3 << 27);
     }
-    bot_pair<kList, L8, LAZY>(st, x, Tf56, 0, Tg5, Vhi, 0, fr >> 4, gl, gbase, L, lane, sel, sstride, c);  // leaves 4, 5
-    if constexpr (LAZY) prefetch_next();
+    bot_pair<kList, L8>(st, x, Tf56, 0, Tg5, Vhi, 0, fr >> 4, gl, gbase, L, lane, sel, sstride, c);  // leaves 4, 5
 #pragma unroll
     for (int s = 0; s < NS; ++s) {  // q2: W1 = g(W2, c2)
         x[s][1] = (x[s][1] & ~(3u << 25)) | (c[s] << 25);
         x[s][1] = (x[s][1] & ~(0xffu << 16)) | (g_pair(Tg2, c[s], x[s][1] & 0xffffu) << 16);
     }
-    bot_pair<kList, L8, LAZY>(st, x, Tf56, 256, Tg6, Vhi, 32, fr >> 6, gl, gbase, L, lane, sel, sstride, c);  // leaves 6, 7
+    bot_pair<kList, L8>(st, x, Tf56, 256, Tg6, Vhi, 32, fr >> 6, gl, gbase, L, lane, sel, sstride, c);  // leaves 6, 7
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const uint32_t c2 = (x[s][1] >> 25) & 3u;
@@ -772,9 +663,9 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
         const uint32_t c3l = (x[s][1] >> 27) & 15u;
         uint32_t res = (c3l ^ c3r) | (c3r << 4);  // combine at depth n-3
         if (op.flags & MF_BCOMB)  // and the parent's (utils.cpp:62-67): U[n-3] of this lineage ^ res | res
-            res = ((M[s].ld(op.flags & MF_U_LDS, op.u_row, gbase + pfield(st[s].U(), op.sh_u)) & 0xFFu) ^ res) | (res << 8);
+            res = ((M[s].ld(op.flags & MF_U_LDS, op.u_row, gbase + pfield(st[s].pu, op.sh_u)) & 0xFFu) ^ res) | (res << 8);
         M[s].st(op.flags & MF_DST_LDS, op.dst_row, lane, res);
-        if (!(op.flags & MF_TO_R)) st[s].U() = pset(st[s].U(), op.sh_dst, gl);
+        if (!(op.flags & MF_TO_R)) st[s].pu = pset(st[s].pu, op.sh_dst, gl);
     }
 }
 
@@ -787,13 +678,11 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
 // ---------------------------------------------------------------------------
 
 // LDS view of the R1 argsort array: 16-bit entries (rank << 5 | element),
-// entry p of this lane at row base + p/2, half p%2 of the lane's dword (rows
-// `hs` halfwords apart: the set-interleaved row stride, see Mem).
+// entry p of this lane at row base + p/2, half p%2 of the lane's dword.
 struct LdsSeq16 {
     uint16_t *lane0;  // &row[base][lane] as 16-bit
-    int hs;
-    __device__ __forceinline__ int get(int p) const { return lane0[(p >> 1) * hs + (p & 1)]; }
-    __device__ __forceinline__ void set(int p, int e) const { lane0[(p >> 1) * hs + (p & 1)] = (uint16_t)e; }
+    __device__ __forceinline__ int get(int p) const { return lane0[(p >> 1) * 128 + (p & 1)]; }
+    __device__ __forceinline__ void set(int p, int e) const { lane0[(p >> 1) * 128 + (p & 1)] = (uint16_t)e; }
     __device__ __forceinline__ bool less(int a, int b) const { return (a >> 5) < (b >> 5); }  // keys only, as std::sort
 };
 
@@ -806,8 +695,8 @@ struct LdsSeq16 {
 // by shuffles; each lane re-derives its own entry's magnitude, a quanta-row
 // lookup or a vcl read), and its flips are one bit mask (temp <= 32) shuffled
 // with the survivors.  Returns the node's bits.
-template <bool L8, class Path>
-__device__ __forceinline__ uint32_t r1_layers(Path &st, int *sel, int sj, int gl, int gbase, int lane, int L, int m,
+template <bool L8>
+__device__ __forceinline__ uint32_t r1_layers(Path &st, int *sel, int gl, int gbase, int lane, int L, int m,
                                                      uint32_t ordp0, uint32_t ordp1, uint32_t symp, bool uni,
                                                      double vrow, const double *vq, int v, uint32_t hw, int temp) {
     uint32_t flips = 0;
@@ -828,11 +717,12 @@ __device__ __forceinline__ uint32_t r1_layers(Path &st, int *sel, int sj, int gl
             if constexpr (L8)
                 if (keep_all8(__builtin_bit_cast(uint64_t, st.pm), __builtin_bit_cast(uint64_t, kf), gl)) break;
             const int pos_old = lane_read(own, o);  // H2
-            const Sel sl = L8 ? select_survivors8(st.pm, kf, gl, gbase, lane, sel, sj)
+            const Sel sl = L8 ? select_survivors8(st.pm, kf, gl, gbase, lane, sel)
                               : select_survivors(st.pm, kf, gl, gbase, L, sel);
             const int p = gbase + sl.parent;
             st.pm = pick(sl.upper, shfld(kf, p), shfld(st.pm, p));
-            st.move(p);
+            st.ps = shfl64(st.ps, p);
+            st.pu = shfl64(st.pu, p);
             origin = lane_read(origin, p);
             flips = (uint32_t)lane_read((int)flips, p) ^ (sl.upper ? 1u << (pos_old & 31) : 0u);
         }
@@ -841,9 +731,9 @@ __device__ __forceinline__ uint32_t r1_layers(Path &st, int *sel, int sj, int gl
     return temp < 32 ? word & ((1u << temp) - 1u) : word;
 }
 
-template <bool L8, class Path>
-__device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const MOp &op, Path &st, int *sel, int sj,
-                                         int gl, int gbase, int L, int lane, int temp) {
+template <bool L8>
+__device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const MOp &op, Path &st, int *sel, int gl,
+                                         int gbase, int L, int lane, int temp) {
     const int src = gbase + pfield(st.ps, op.sh_src);
     const bool sl = op.flags & MF_SRC_LDS;
     const int v = P.v;
@@ -905,7 +795,7 @@ __device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const 
             }
         }
     } else {
-        const LdsSeq16 seq{(uint16_t *)(M.lds + M.rw(op.u_row) + lane), M.ns * 128};
+        const LdsSeq16 seq{(uint16_t *)(M.lds + op.u_row * 64 + lane)};
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
             if (j < temp) {
@@ -933,13 +823,12 @@ __device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const 
         }
     }
     const uint32_t word =
-        r1_layers<L8>(st, sel, sj, gl, gbase, lane, L, m, ordp0, ordp1, symp, uni, vrow, vq, v, hw, temp);
+        r1_layers<L8>(st, sel, gl, gbase, lane, L, m, ordp0, ordp1, symp, uni, vrow, vq, v, hw, temp);
     M.st(op.flags & MF_DST_LDS, op.dst_row, lane, word);
 }
 
 // R1 nodes above 32 elements (N >= 2048 codes) or without LDS room: the
 // argsort arrays live in the wave's global slab (H / K / I rows).
-template <class Path>
 __device__ __forceinline__ void r1_large(const FastPlan &P, const Mem &M, const MOp &op, Path &st, int *sel, int gl,
                                       int gbase, int L, int lane, int temp) {
     const int src = gbase + pfield(st.ps, op.sh_src);
@@ -958,11 +847,9 @@ __device__ __forceinline__ void r1_large(const FastPlan &P, const Mem &M, const 
             const int j = 32 * w + i;
             const double l = llr(j);
             word |= (uint32_t)(l < 0) << i;
-            const uint64_t b = __builtin_bit_cast(uint64_t, fabs(l));
-            g[(size_t)M.rw(P.K_row + 2 * j) + lane] = (uint32_t)b;
-            g[(size_t)M.rw(P.K_row + 2 * j + 1) + lane] = (uint32_t)(b >> 32);
+            ((double *)(g + (size_t)(P.K_row + 2 * j) * 64))[lane] = fabs(l);
         }
-        g[(size_t)M.rw(P.H_row + w) + lane] = word;
+        g[(size_t)(P.H_row + w) * 64 + lane] = word;
     }
     int ord[kMaxM];
     double ms[kMaxM];
@@ -972,7 +859,7 @@ __device__ __forceinline__ void r1_large(const FastPlan &P, const Mem &M, const 
         ms[q] = 0;
         flip[q] = -1;
     }
-    FastSortSeq seq{g, P.I_row, P.K_row, lane, M.ns * 64};
+    FastSortSeq seq{g, P.I_row, P.K_row, lane};
     for (int p = 0; p < temp; ++p) seq.set(p, p);
     stl::sort(seq, 0, temp);
     for (int q = 0; q < kMaxM; ++q) {
@@ -990,7 +877,8 @@ __device__ __forceinline__ void r1_large(const FastPlan &P, const Mem &M, const 
             const int p = gbase + sx.parent;
             const int pos_old = ord[layer];  // H2
             st.pm = pick(sx.upper, shfld(kf, p), shfld(st.pm, p));
-            st.move(p);
+            st.ps = shfl64(st.ps, p);
+            st.pu = shfl64(st.pu, p);
             origin = lane_read(origin, p);
             for (int q = 0; q < kMaxM; ++q) {
                 ord[q] = lane_read(ord[q], p);
@@ -1001,7 +889,7 @@ __device__ __forceinline__ void r1_large(const FastPlan &P, const Mem &M, const 
         }
     }
     for (int w = 0; w < nwo; ++w) {
-        uint32_t word = g[(size_t)M.rw(P.H_row + w) + gbase + origin];
+        uint32_t word = g[(size_t)(P.H_row + w) * 64 + gbase + origin];
         for (int q = 0; q < kMaxM; ++q)
             if (q < m && flip[q] >= 0 && (flip[q] >> 5) == w) word ^= 1u << (flip[q] & 31);
         if (temp < 32) word &= (1u << temp) - 1u;
@@ -1013,9 +901,9 @@ __device__ __forceinline__ void r1_large(const FastPlan &P, const Mem &M, const 
 // without LDS room; N >= 2048 codes).  Only those plans get it compiled in:
 // its argsort stack and arrays cost the other instantiations registers and
 // scratch (+3 % FastSCL-LUT at N = 1024 without it).
-template <bool kList, bool L8, bool R1L, class Path>
-__device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, const MOp &op, Path &st, int *sel, int sj,
-                                           int gl, int gbase, int L, int lane) {
+template <bool kList, bool L8, bool R1L>
+__device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, const MOp &op, Path &st, int *sel, int gl,
+                                           int gbase, int L, int lane) {
     const int fl = op.flags;
     const int temp = op.cnt;
     const int src = gbase + pfield(st.ps, op.sh_src);
@@ -1080,10 +968,11 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
             if (L8 && keep_all8(__builtin_bit_cast(uint64_t, kk), __builtin_bit_cast(uint64_t, kf), gl)) {
                 st.pm = kk;  // identity selection: every path keeps its all-zeros codeword
             } else {
-                const Sel sx = L8 ? select_survivors8(kk, kf, gl, gbase, lane, sel, sj) : select_survivors(kk, kf, gl, gbase, L, sel);
+                const Sel sx = L8 ? select_survivors8(kk, kf, gl, gbase, lane, sel) : select_survivors(kk, kf, gl, gbase, L, sel);
                 const int p = gbase + sx.parent;
                 st.pm = pick(sx.upper, shfld(kf, p), shfld(kk, p));
-                st.move(p);
+                st.ps = shfl64(st.ps, p);
+                st.pu = shfl64(st.pu, p);
                 fill = sx.upper ? 0xffffffffu : 0u;
             }
         }
@@ -1135,11 +1024,11 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
             }
         }
     } else if (temp <= stl::kThreshold || (fl & MF_R1_LDS)) {
-        r1_small<L8>(P, M, op, st, sel, sj, gl, gbase, L, lane, temp);
+        r1_small<L8>(P, M, op, st, sel, gl, gbase, L, lane, temp);
     } else if constexpr (R1L) {
         r1_large(P, M, op, st, sel, gl, gbase, L, lane, temp);
     }
-    if (!(fl & MF_TO_R)) st.U() = pset(st.U(), op.sh_dst, gl);
+    if (!(fl & MF_TO_R)) st.pu = pset(st.pu, op.sh_dst, gl);
 }
 
 #ifdef QPD_STAMPS
@@ -1149,7 +1038,7 @@ __device__ unsigned long long qpd_stamp_acc[64];
 #endif
 
 // Waves per SIMD the register allocation targets: 6 (80 VGPRs) for one
-// frame set, 4 (128 VGPRs) for two (5 for SCL-LUT, below), 6 for FastSCL's one set too (its special
+// frame set, 4 (128 VGPRs) for two, 6 for FastSCL's one set too (its special
 // ops spill ~136 B at 80 VGPRs, yet with the task queue 6 waves beat 5 by 4%)
 // -- the measured optima on MI355X.
 #ifndef QPD_WPE1
@@ -1161,20 +1050,12 @@ __device__ unsigned long long qpd_stamp_acc[64];
 #ifndef QPD_WPE2
 #define QPD_WPE2 4
 #endif
-// SCL-LUT's two-set decode kernel: 5 waves per SIMD (96 VGPRs) since its path
-// state takes one pointer word (PW1) and its BOT3 stages its loads (r04h:
-// 44.3 vs 41.7 M frames/s at 4 waves)
-#ifndef QPD_WPE2_SCL
-#define QPD_WPE2_SCL 5
-#endif
 #ifndef QPD_WPE3
 #define QPD_WPE3 3
 #endif
 // NS frame sets per wave (see above); L8: list decoders with L = 8.
-// LDS: NS * (lds_rows + 2) rows, set-interleaved (see Mem): a set's rows
-// 0..lds_rows-1 (grouped by depth, see FastLayout), then its selection scratch
-// as rows lds_rows (64 slots) and lds_rows + 1 (junk slots).
-// Global slab: NS * glb_rows rows per workgroup, set-interleaved.
+// LDS: NS * kSelInts ints of selection scratch, then NS * lds_rows rows.
+// Global slab: NS * glb_rows rows per workgroup.
 // PFX: the frozen-prefix kernel (lut_prefix_kernel below; one set, gs = 1, no
 // tail, `out` unused).  A template argument rather than a wrapper around a
 // shared body: the wrapper moved the decode kernels' register allocation
@@ -1183,35 +1064,21 @@ __device__ unsigned long long qpd_stamp_acc[64];
 // `ops` is its own __restrict__ argument (= P.ops) so that the compiler can
 // prove the op records are never written and fetch them with scalar loads
 // instead of vector loads + readfirstlane, which drain vmcnt at every op.
-// PW1: one pointer word per path (PathT; the host packed the op list's fields).
-template <int KIND, int NS, bool L8, bool R1L = false, bool PFX = false, bool PW1 = false>
-__global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
-                                : NS == 2 ? (KIND == K_SCL_LUT && !PFX ? QPD_WPE2_SCL : QPD_WPE2)
-                                : KIND == K_FASTSCL_LUT ? QPD_WPE_FSCL : QPD_WPE1) void lut_fast_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
+template <int KIND, int NS, bool L8, bool R1L = false, bool PFX = false>
+__global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3 : NS == 2 ? QPD_WPE2 : KIND == K_FASTSCL_LUT ? QPD_WPE_FSCL : QPD_WPE1) void lut_fast_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
                                                                uint8_t *__restrict__ out,
                                                                const MOp *__restrict__ ops) {
     constexpr bool kList = (KIND == K_SCL_LUT || KIND == K_FASTSCL_LUT);
-    // staged BOT3 loads + the speculative right-leaf lookup: SCL-LUT (the
-    // FastSCL-LUT unit measured 15-25 % slower with them, r04h)
-    constexpr bool kLazy = QPD_BOT3_LAZY && KIND == K_SCL_LUT;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
-    // rows of all sets interleaved, each set's selection scratch as its next two
-    // rows: set s's slots at sel_all + s * 64, its junk slots NS * 64 words on
-    const int sstride = 64;
-    int *const sel_all = (int *)(lds_dyn + NS * P.lds_rows * 64);
+    // per set: [lds_rows rows][selection scratch] (rows grouped by depth, see FastLayout)
+    const int sstride = P.lds_rows * 64 + kSelInts;
+    int *const sel_all = (int *)(lds_dyn + P.lds_rows * 64);
     Mem Mv[NS];
-    {
-        uint32_t *const slab = P.scratch + (size_t)blockIdx.x * NS * P.glb_rows * 64;
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(slab, 0, NS * P.glb_rows * 256 * QPD_EXP_SLABMUL, 0x00020000);
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            Mv[s].lds = lds_dyn + s * 64;
-            Mv[s].gp = slab + s * 64;
-            Mv[s].rs = rs;
-            Mv[s].so = s * 256;
-            Mv[s].ns = NS;
-        }
+    for (int s = 0; s < NS; ++s) {
+        Mv[s].lds = lds_dyn + s * sstride;
+        Mv[s].gp = P.scratch + ((size_t)blockIdx.x * NS + s) * P.glb_rows * 64;
+        Mv[s].rs = __builtin_amdgcn_make_buffer_rsrc(Mv[s].gp, 0, P.glb_rows * 256 * QPD_EXP_SLABMUL, 0x00020000);
     }
     const int gs = P.gs;
     const int L = kList ? P.L : 1;
@@ -1229,11 +1096,13 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
         // Diagnosis builds only: every LDS word and slab row of this wave set to
         // QPD_POISON at the start of each task, so that a read of a row no op of
         // this task wrote shows up as a parity difference.
-        for (int i = threadIdx.x; i < NS * (P.lds_rows * 64 + kSelInts); i += 64) lds_dyn[i] = (uint32_t)QPD_POISON;
-        for (int r = 0; r < NS * P.glb_rows; ++r) Mv[0].gp[r * 64 + threadIdx.x] = (uint32_t)QPD_POISON;
+        for (int i = threadIdx.x; i < NS * sstride; i += 64) lds_dyn[i] = (uint32_t)QPD_POISON;
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+            for (int r = 0; r < P.glb_rows; ++r) Mv[s].gp[r * 64 + threadIdx.x] = (uint32_t)QPD_POISON;
         wave_sync();
 #endif
-        PathT<PW1> stv[NS];
+        Path stv[NS];
         {
             const int lane = threadIdx.x, gl = lane & (gs - 1);
             uint64_t self = 0;
@@ -1242,7 +1111,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
             for (int s = 0; s < NS; ++s) {
                 stv[s].pm = (gl == 0) ? 0.0 : kInf;
                 stv[s].ps = self;
-                stv[s].U() = self;  // (PW1: the same word)
+                stv[s].pu = self;
             }
         }
 #ifdef QPD_STAMPS
@@ -1279,17 +1148,14 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
             __builtin_amdgcn_s_waitcnt(0);
             const uint64_t stamp_t0 = __builtin_amdgcn_s_memtime();
 #endif
-            // the next op's operands; a BOT3 issues them itself, late (see bot3_op)
             if (oi + 1 < P.nops) {
                 nxt = ops[oi + 1];
-                if (!kLazy || op.type != OP_BOT3) pre = fetch_pre(P, nxt, lane, vlane);
+                pre = fetch_pre(P, nxt, lane, vlane);
             }
             const int fl = op.flags;
             switch (op.type) {
                 case OP_BOT3:
-                    bot3_op<kList, L8, kLazy>(P, Mv, op, yv, stv, cur.T, cur.T2, gl, gbase, L, sel_all, sstride, lane, [&]() {
-                        if (oi + 1 < P.nops) pre = fetch_pre(P, nxt, lane, vlane);
-                    });
+                    bot3_op<kList, L8>(P, Mv, op, yv, stv, cur.T, cur.T2, gl, gbase, L, sel_all, sstride, lane);
                     break;
                 case OP_F:
                 case OP_G: {
@@ -1297,7 +1163,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
 #pragma unroll
                     for (int s = 0; s < NS; ++s) {
                         src[s] = gbase + pfield(stv[s].ps, op.sh_src);
-                        usrc[s] = gbase + pfield(stv[s].U(), op.sh_u);
+                        usrc[s] = gbase + pfield(stv[s].pu, op.sh_u);
                     }
                     if (fl & MF_GSEL)
                         gsel_op(Mv, op, yv, usrc, lane);
@@ -1331,7 +1197,6 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                     const bool frozen = op.cnt != 0;
                     double dm[NS];
                     uint32_t none[NS][1], dec[NS];
-                    bool moved[NS];
 #pragma unroll
                     for (int s = 0; s < NS; ++s) {
                         dm[s] = 0;
@@ -1340,15 +1205,15 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                             const uint32_t W = sym_word(P, Mv[s], op, yv[s], gbase + pfield(stv[s].ps, op.sh_src), 0, 2);
                             uint32_t idx = ((W & 15u) << 4) | ((W >> 4) & 15u);
                             if (right)
-                                idx |= (Mv[s].ld(fl & MF_U_LDS, op.u_row, gbase + pfield(stv[s].U(), op.sh_u)) & 1u) << 8;
+                                idx |= (Mv[s].ld(fl & MF_U_LDS, op.u_row, gbase + pfield(stv[s].pu, op.sh_u)) & 1u) << 8;
                             dm[s] = shfld(cur.V, (int)lut4(cur.T, idx));  // vcl[n-1][k][s] (H3)
                         }
                     }
-                    leaf_decide<kList, L8>(stv, dm, frozen, gl, gbase, L, lane, sel_all, sstride, none, dec, moved);
+                    leaf_decide<kList, L8>(stv, dm, frozen, gl, gbase, L, lane, sel_all, sstride, none, dec);
 #pragma unroll
                     for (int s = 0; s < NS; ++s) {
                         Mv[s].st(fl & MF_DST_LDS, op.dst_row, lane, dec[s]);
-                        if (!right) stv[s].U() = pset(stv[s].U(), op.sh_dst, gl);
+                        if (!right) stv[s].pu = pset(stv[s].pu, op.sh_dst, gl);
                     }
                     break;
                 }
@@ -1360,7 +1225,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                         uint32_t u[NS], r[NS];
 #pragma unroll
                         for (int s = 0; s < NS; ++s) {
-                            u[s] = Mv[s].ld(ul, op.u_row, gbase + pfield(stv[s].U(), op.sh_u)) & m;
+                            u[s] = Mv[s].ld(ul, op.u_row, gbase + pfield(stv[s].pu, op.sh_u)) & m;
                             r[s] = Mv[s].ld(rl, op.r_row, lane) & m;
                         }
 #pragma unroll
@@ -1369,7 +1234,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                         const int cw = ctemp >> 5;  // 1, 2 or a multiple of 4
                         int usrc[NS];
 #pragma unroll
-                        for (int s = 0; s < NS; ++s) usrc[s] = gbase + pfield(stv[s].U(), op.sh_u);
+                        for (int s = 0; s < NS; ++s) usrc[s] = gbase + pfield(stv[s].pu, op.sh_u);
                         // 4 words of every set per round: all their loads in flight together
                         for (int w0 = 0; w0 < cw; w0 += 4) {
                             uint32_t u[NS][4], r[NS][4];
@@ -1395,7 +1260,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                     }
                     if (!(fl & MF_TO_R)) {
 #pragma unroll
-                        for (int s = 0; s < NS; ++s) stv[s].U() = pset(stv[s].U(), op.sh_dst, gl);
+                        for (int s = 0; s < NS; ++s) stv[s].pu = pset(stv[s].pu, op.sh_dst, gl);
                     }
                     break;
                 }
@@ -1431,7 +1296,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                         for (int s = 0; s < NS; ++s) {
                             const int64_t f = (task * NS + s) * fpw + (lane >> gsh);
                             const int at = (fl & MF_VIA_PS)   ? gbase + pfield(stv[s].ps, op.sh_src)
-                                           : (fl & MF_VIA_PU) ? gbase + pfield(stv[s].U(), op.sh_src)
+                                           : (fl & MF_VIA_PU) ? gbase + pfield(stv[s].pu, op.sh_src)
                                                               : lane;
                             const int G = P.pfx_geo & 255;
                             uint32_t *dst = P.pfx + (((f >> G) * P.pfx_rec) << 6) + ((f & ((1 << G) - 1)) << (P.pfx_geo >> 8)) + gl;
@@ -1443,12 +1308,11 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                     }
                     break;
                 default: if constexpr (KIND == K_FASTSC_LUT || KIND == K_FASTSCL_LUT) {  // special nodes, FastSCLUT.cpp:46-107 / FastSCLLUTDecoder.cpp:82-213
-#pragma unroll
                   for (int s = 0; s < NS; ++s) {
-                    auto &st = stv[s];
+                    Path &st = stv[s];
                     const Mem &M = Mv[s];
                     int *const sel = sel_all + sstride * s;
-                    special_op<kList, L8, R1L>(P, M, op, st, sel, NS * sstride, gl, gbase, L, lane);
+                    special_op<kList, L8, R1L>(P, M, op, st, sel, gl, gbase, L, lane);
                   }
                   break;
                 }
@@ -1559,14 +1423,14 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                         }
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
-                    if (k < wpl) M.lds[M.rw(k) + lane] = x[k];  // word gl*wpl + k at row k, column lane
+                    if (k < wpl) M.lds[k * 64 + lane] = x[k];  // word gl*wpl + k at row k, column lane
                 wave_sync();
             }
             const int64_t frame = (task * NS + s) * fpw + lane / gs;
             if (frame < B) {
                 auto bit = [&](int pos) {
                     const int w = pos >> 5;
-                    const uint32_t x = split ? M.lds[M.rw(w & (wpl - 1)) + gbase + (w >> wsh)] : M.ldv(rl, r0 + w, src);
+                    const uint32_t x = split ? M.lds[(w & (wpl - 1)) * 64 + gbase + (w >> wsh)] : M.ldv(rl, r0 + w, src);
                     return (x >> (pos & 31)) & 1u;
                 };
                 if (dword_out) {
@@ -1630,7 +1494,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
 // accumulated by the same code in the same leaf order, so the doubles are
 // identical.
 // ---------------------------------------------------------------------------
-#define lut_prefix_kernel(KIND, NS, PW1) lut_fast_kernel<KIND, NS, false, false, true, PW1>
+#define lut_prefix_kernel(KIND, NS) lut_fast_kernel<KIND, NS, false, false, true>
 
 #ifndef QPD_FAST_TEMPLATES_ONLY  // qpd_fast_fscl.hip: the decode kernel templates only
 // ---------------------------------------------------------------------------
@@ -1675,4 +1539,5 @@ __global__ __launch_bounds__(256) void root_pre_kernel(FastPlan P, const int32_t
 }
 #endif  // QPD_FAST_TEMPLATES_ONLY
 
+}  // namespace fscl
 }  // namespace qpd
