@@ -38,9 +38,11 @@ disp = collections.defaultdict(lambda: collections.defaultdict(set))
 short = {"lut_fast_kernel": "lut_fast_kernel", "root_pre_kernel": "root_pre_kernel",
          "generic_decode_kernel": "generic_decode_kernel", "mc_frames_kernel": "mc_frames_kernel"}
 def kernel_of(full):
-    # lut_fast_kernel<KIND, 1, false, false, true>: the frozen-prefix instantiation (PFX)
-    if "lut_fast_kernel" in full and "true>(" in full.replace(" ", ""):
-        return "lut_prefix_kernel"
+    # lut_fast_kernel<KIND, NS, L8, R1L, PFX[, PW1]>: PFX true = the frozen-prefix stages
+    if "lut_fast_kernel<" in full:
+        args = full.split("lut_fast_kernel<", 1)[1].split(">", 1)[0].replace(" ", "").split(",")
+        if len(args) >= 5 and args[4] == "true":
+            return "lut_prefix_kernel"
     return next((s for s in short if s in full), None)
 
 

@@ -9,7 +9,8 @@ for path in sys.argv[2:]:
     nd = set()
     for r in csv.DictReader(open(path)):
         kn = r["Kernel_Name"]
-        if ("lut_fast_kernel" in kn and "true>(" not in kn.replace(" ", "")) or "lut_decode_kernel" in kn:  # not the prefix
+        args = kn.split("lut_fast_kernel<", 1)[1].split(">", 1)[0].replace(" ", "").split(",") if "lut_fast_kernel<" in kn else []
+        if (args and not (len(args) >= 5 and args[4] == "true")) or "lut_decode_kernel" in kn:  # not the prefix (PFX)
             agg[r["Counter_Name"]] += float(r["Counter_Value"])
             nd.add(r["Dispatch_Id"])
     print(f"# {path} ({len(nd)} dispatch(es))")
