@@ -480,6 +480,71 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
     out.push_back(m);
 }
 
+// Fold an F at depth d+1 into the F / G right before it that produced its
+// input (MF_FF, ff_op in qpd_fast.hip): the child's f reads the words the
+// parent just computed from registers instead of re-reading S[d+1] from the
+// slab.  Pairs are taken greedily down each descent (G1+F2, F3+F4, ...);
+// S[d] and S[d+1] as the slab rows ff_op reads, S[d+1] of at least 4 words.
+// The rows written are the same as before, so the prefix split's analysis
+// (op_rows on the unfused list) and the stores' order are unchanged.
+void fuse_descent(std::vector<qpd::MOp> &ops) {
+    using namespace qpd;
+    std::vector<MOp> out;
+    out.reserve(ops.size());
+    for (size_t i = 0; i < ops.size(); ++i) {
+        MOp a = ops[i];
+        if (i + 1 < ops.size() && (a.type == OP_F || a.type == OP_G) &&
+            !(a.flags & (MF_CHAN | MF_PRE | MF_GSEL | MF_SRC_LDS | MF_FF)) && a.cnt >= 32) {
+            const MOp &b = ops[i + 1];
+            const bool dl = a.flags & MF_DST_LDS, cdl = b.flags & MF_DST_LDS;
+            if (b.type == OP_F && b.d == a.d + 1 && b.src_row == a.dst_row && b.sh_src == a.sh_dst &&
+                ((b.flags & MF_SRC_LDS) != 0) == dl && !(dl && !cdl) && !(b.flags & (MF_CHAN | MF_PRE | MF_GSEL)) &&
+                b.cnt * 2 == a.cnt) {
+                a.flags |= MF_FF | (cdl ? MF_FF_DL : 0);
+                a.r_row = b.dst_row;
+                a.tab2 = b.tab;
+                a.pad1 = b.sh_dst;
+                out.push_back(a);
+                ++i;
+                continue;
+            }
+        }
+        out.push_back(a);
+    }
+    ops.swap(out);
+}
+
+// Fold the combine at depth n-5 into the right BOT3 before it (MF_BC2, the
+// end of bot3_op in qpd_fast.hip): a right BOT3 that already runs its
+// parent's combine (MF_BCOMB) and writes R[n-4] is followed by the COMB that
+// reads that row and its left sibling's U[n-4]; the BOT3 computes that
+// combine from its result in registers and writes the COMB's destination, so
+// R[n-4] is neither stored nor loaded and the COMB op goes.  SCL-LUT only.
+void fold_combine(std::vector<qpd::MOp> &ops) {
+    using namespace qpd;
+    std::vector<MOp> out;
+    out.reserve(ops.size());
+    for (size_t i = 0; i < ops.size(); ++i) {
+        MOp a = ops[i];
+        if (i + 1 < ops.size() && a.type == OP_BOT3 && (a.flags & MF_BCOMB) && (a.flags & MF_TO_R) && !(a.flags & MF_BC2)) {
+            const MOp &b = ops[i + 1];
+            if (b.type == OP_COMB && b.d == a.d - 2 && b.cnt == 16 && b.r_row == a.dst_row &&
+                ((b.flags & MF_R_LDS) != 0) == ((a.flags & MF_DST_LDS) != 0) && b.sh_u < 256 && b.sh_dst < 256 &&
+                b.dst_row >= 0 && b.dst_row < 32768) {
+                a.flags |= MF_BC2 | ((b.flags & MF_U_LDS) ? MF_BC2_ULDS : 0) | ((b.flags & MF_DST_LDS) ? MF_BC2_DLDS : 0) |
+                           ((b.flags & MF_TO_R) ? MF_BC2_TOR : 0);
+                a.r_row = b.u_row;
+                a.pad1 = b.sh_u | (b.sh_dst << 8) | (b.dst_row << 16);
+                out.push_back(a);
+                ++i;
+                continue;
+            }
+        }
+        out.push_back(a);
+    }
+    ops.swap(out);
+}
+
 // Place the global-slab drains (MF_SYNC: vmcnt(0) + barrier BEFORE the op).
 // A path reads another path's slab rows only through pointer fields copied
 // at a fork, and every op that writes a depth's rows writes all lanes' own
@@ -506,15 +571,17 @@ void place_syncs(std::vector<qpd::MOp> &ops, bool list) {
             default: break;
         }
         const bool src_glb = !(m.flags & (MF_SRC_LDS | MF_CHAN | MF_PRE));
-        const bool u_glb = (m.type == OP_G || m.type == OP_COMB || m.type == OP_LEAF_R ||
-                            (m.type == OP_BOT3 && (m.flags & (MF_BG | MF_BCOMB)))) &&
-                           !(m.flags & MF_U_LDS);
-        const bool late_u = m.type == OP_BOT3 && (m.flags & MF_BCOMB) && !(m.flags & MF_U_LDS) && forks;
+        const bool u_glb = ((m.type == OP_G || m.type == OP_COMB || m.type == OP_LEAF_R ||
+                             (m.type == OP_BOT3 && (m.flags & (MF_BG | MF_BCOMB)))) &&
+                            !(m.flags & MF_U_LDS)) ||
+                           (m.type == OP_BOT3 && (m.flags & MF_BC2) && !(m.flags & MF_BC2_ULDS));
+        const bool late_u = m.type == OP_BOT3 && forks &&
+                            (((m.flags & MF_BCOMB) && !(m.flags & MF_U_LDS)) || ((m.flags & MF_BC2) && !(m.flags & MF_BC2_ULDS)));
         if ((exposed && (src_glb || u_glb)) || (late_u && dirty)) {
             m.flags |= MF_SYNC;
             exposed = dirty = false;
         }
-        if (!(m.flags & MF_DST_LDS)) dirty = true;
+        if (!(m.flags & ((m.type == OP_BOT3 && (m.flags & MF_BC2)) ? MF_BC2_DLDS : MF_DST_LDS))) dirty = true;
         if (forks && dirty) exposed = true;
     }
 }
@@ -554,6 +621,7 @@ void op_rows(const qpd::MOp &m, Fn &&acc) {
             if (src_row) acc(false, sp_s, m.src_row, c >= 8 ? 2 * (c >> 3) : 1);
             if (m.type == OP_G) acc(false, sp_u, m.u_row, std::max(1, c >> 5));
             acc(true, sp_d, m.dst_row, c >= 8 ? c >> 3 : 1);
+            if (fl & MF_FF) acc(true, (fl & MF_FF_DL) ? 1 : 0, m.r_row, c >> 4);
             break;
         case OP_COMB: {
             const int cw = c < 32 ? 1 : c >> 5;
@@ -571,7 +639,12 @@ void op_rows(const qpd::MOp &m, Fn &&acc) {
         case OP_BOT3:
             if (src_row) acc(false, sp_s, m.src_row, (fl & MF_BFG) ? 2 : 1);
             if (fl & (MF_BG | MF_BCOMB)) acc(false, sp_u, m.u_row, 1);
-            acc(true, sp_d, m.dst_row, 1);
+            if (fl & MF_BC2) {
+                acc(false, (fl & MF_BC2_ULDS) ? 1 : 0, m.r_row, 1);
+                acc(true, (fl & MF_BC2_DLDS) ? 1 : 0, m.pad1 >> 16, 1);
+            } else {
+                acc(true, sp_d, m.dst_row, 1);
+            }
             break;
         case OP_IMPORT: acc(true, sp_d, m.dst_row, c); break;
         case OP_EXPORT: acc(false, sp_s, m.src_row, c); break;
@@ -852,6 +925,7 @@ bool compact_pointer_fields(const std::vector<std::vector<qpd::MOp> *> &lists) {
     int pos[2][kMaxDepth + 1];
     for (auto &a : pos)
         for (int &x : a) x = -1;
+    int bc_u = 0, bc_dst = 0;  // an MF_BC2 op's two fields (pad1), unpacked before each()
     auto each = [&](qpd::MOp &m, auto &&fn) {  // fn(slot 0 = S / 1 = U, int &sh)
         const int fl = m.flags;
         const bool src_row = !(fl & (MF_CHAN | MF_PRE));
@@ -861,6 +935,7 @@ bool compact_pointer_fields(const std::vector<std::vector<qpd::MOp> *> &lists) {
                 if (src_row) fn(0, m.sh_src);
                 if (m.type == OP_G) fn(1, m.sh_u);  // (MF_GSEL reads U[1] through it too)
                 fn(0, m.sh_dst);
+                if (fl & MF_FF) fn(0, m.pad1);
                 break;
             case OP_LEAF_L:
             case OP_LEAF_R:
@@ -876,6 +951,10 @@ bool compact_pointer_fields(const std::vector<std::vector<qpd::MOp> *> &lists) {
                 if (src_row) fn(0, m.sh_src);
                 if (fl & (MF_BG | MF_BCOMB)) fn(1, m.sh_u);
                 if (!(fl & MF_TO_R)) fn(1, m.sh_dst);
+                if (fl & MF_BC2) {  // (the fields packed in pad1, unpacked into bc_u / bc_dst)
+                    fn(1, bc_u);
+                    if (!(fl & MF_BC2_TOR)) fn(1, bc_dst);
+                }
                 break;
             case OP_IMPORT: break;
             case OP_EXPORT:
@@ -888,10 +967,14 @@ bool compact_pointer_fields(const std::vector<std::vector<qpd::MOp> *> &lists) {
                 break;
         }
     };
+    auto unpack = [&](const qpd::MOp &m) {
+        bc_u = m.pad1 & 255;
+        bc_dst = (m.pad1 >> 8) & 255;
+    };
     int used = 0;
     for (auto *l : lists)
         for (qpd::MOp &m : *l)
-            each(m, [&](int sl, int &sh) {
+            unpack(m), each(m, [&](int sl, int &sh) {
                 int &p = pos[sl][sh / 4];
                 if (p < 0) p = used++;
             });
@@ -900,16 +983,23 @@ bool compact_pointer_fields(const std::vector<std::vector<qpd::MOp> *> &lists) {
         for (qpd::MOp &m : *l) {
             // every field of an op is rewritten once (fields shared by two
             // roles, e.g. sh_src of a special node, are read before any write)
-            int sh_src = m.sh_src, sh_u = m.sh_u, sh_dst = m.sh_dst;
+            int sh_src = m.sh_src, sh_u = m.sh_u, sh_dst = m.sh_dst, pad1 = m.pad1;
+            unpack(m);
+            int nbc_u = bc_u, nbc_dst = bc_dst;
             each(m, [&](int sl, int &sh) {
                 const int np = 4 * pos[sl][sh / 4];
                 if (&sh == &m.sh_src) sh_src = np;
                 else if (&sh == &m.sh_u) sh_u = np;
+                else if (&sh == &m.pad1) pad1 = np;
+                else if (&sh == &bc_u) nbc_u = np;
+                else if (&sh == &bc_dst) nbc_dst = np;
                 else sh_dst = np;
             });
+            if (m.type == OP_BOT3 && (m.flags & MF_BC2)) pad1 = (m.pad1 & ~0xFFFF) | nbc_u | (nbc_dst << 8);
             m.sh_src = sh_src;
             m.sh_u = sh_u;
             m.sh_dst = sh_dst;
+            m.pad1 = pad1;
         }
     return true;
 }
@@ -1083,15 +1173,28 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
             }
         if (plan_prefix(mops, own, d->L, pp)) mops.swap(pp.rest);
     }
+    d->pfx_sets = std::min(d->sets, 2);
+    // prefix_kernel() instantiates NS = 1 and 2 only: fast_launch's task count
+    // (fgroups) must use the NS the launched kernel has
+    if (const char *e = getenv("QPD_PFX_SETS")) d->pfx_sets = std::min(std::min(d->sets, 2), std::max(1, atoi(e)));
+    // folded descents: the SCL-LUT kernels with two frame sets (ff_op)
+    if (c->kind == QPD_SCL_LUT && !getenv("QPD_NO_FF")) {
+        if (d->sets == 2) fuse_descent(mops);
+        if (d->pfx_sets == 2) {
+            fuse_descent(pp.st1);
+            fuse_descent(pp.st2);
+        }
+    }
+    if (c->kind == QPD_SCL_LUT && !getenv("QPD_NO_BC2")) {  // folded depth n-5 combines (any NS)
+        fold_combine(mops);
+        fold_combine(pp.st1);
+        fold_combine(pp.st2);
+    }
     place_syncs(pp.st1, true);
     place_syncs(pp.st2, true);
     place_syncs(mops, c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT);
     if (c->kind == QPD_SCL_LUT && !getenv("QPD_NO_PW1")) d->pw1 = compact_pointer_fields({&mops, &pp.st1, &pp.st2});
     d->pfx_nops = (int)pp.st1.size();
-    d->pfx_sets = std::min(d->sets, 2);
-    // prefix_kernel() instantiates NS = 1 and 2 only: fast_launch's task count
-    // (fgroups) must use the NS the launched kernel has
-    if (const char *e = getenv("QPD_PFX_SETS")) d->pfx_sets = std::min(std::min(d->sets, 2), std::max(1, atoi(e)));
     d->pfx2_nops = (int)pp.st2.size();
     d->pfx1_rec = pp.rec1;
     d->pfx1_pm = pp.pm1;

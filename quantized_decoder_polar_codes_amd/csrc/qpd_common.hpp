@@ -101,6 +101,7 @@ struct Sel {
 // their composition XOR 4/5/6.
 constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppXor3 = 0x1B, kDppHalfMirror = 0x141;
 constexpr int kDppRowShl1 = 0x101;  // lane i <- lane i+1 within a row of 16
+constexpr int kDppQuadBcast3 = 0xFF;  // quad_perm(3,3,3,3): lane i <- lane 4*(i/4)+3
 
 template <int CTRL>
 __device__ __forceinline__ uint64_t dpp64(uint64_t x) {

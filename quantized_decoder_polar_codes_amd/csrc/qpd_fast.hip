@@ -56,6 +56,17 @@ enum MopFlag : int32_t {
     MF_VIA_PS = 65536,   // OP_EXPORT: the row is read through the path's S pointer of depth sh_src / 4
     MF_VIA_PU = 131072,  //   ... or its U pointer (else the lane's own row: R rows)
     MF_XBUF = 262144,    // OP_IMPORT: from a prefix stage's records (address and layout in the op record)
+    MF_FF = 524288,      // F / G (SCL-LUT) that also runs the f of its left child at depth d+1 from
+                         //   the words it just computed (fuse_descent): S[d+2] at r_row, the
+                         //   child's table at tab2, its S pointer field at pad1
+    MF_FF_DL = 1048576,  //   ... S[d+2] in LDS
+    MF_BC2 = 2097152,    // right BOT3 with MF_BCOMB and MF_TO_R that also runs the combine of its
+                         //   grandparent at depth n-5 (fold_combine): U[n-4] of the left sibling at
+                         //   r_row (pointer field pad1 & 255), result to row pad1 >> 16 (its U
+                         //   pointer field (pad1 >> 8) & 255) instead of R[n-4] at dst_row
+    MF_BC2_ULDS = 4194304,  //   ... that U row in LDS
+    MF_BC2_DLDS = 8388608,  //   ... the result row in LDS
+    MF_BC2_TOR = 16777216,  //   ... the grandparent is a right child (R row: no pointer update)
 };
 
 struct MOp {
@@ -64,14 +75,14 @@ struct MOp {
     int32_t src_row;  // S[d]
     int32_t dst_row;  // F/G: S[d+1]; COMB/special/BOT3: U[d] or R[d]; LEAF_L: U[n]; LEAF_R: R[n]
     int32_t u_row;    // G/COMB: U[d+1]; LEAF_R: U[n]
-    int32_t r_row;    // COMB: R[d+1]
+    int32_t r_row;    // COMB: R[d+1]; F/G with MF_FF: S[d+2]
     int32_t sh_src;   // 4*d: ps field of S[d]
     int32_t sh_u;     // G/COMB: 4*(d+1); LEAF_R: 4*n
     int32_t sh_dst;   // F/G: 4*(d+1) (ps); COMB/special/BOT3 left child: 4*d (pu); LEAF_L: 4*n (pu)
     int32_t tab;      // F/LEAF_L: posi*32; G/LEAF_R: posi*64; BOT3: posi of the subtree root; R1: r1_rank offset
     int32_t vrow;     // LEAF: ((n-1)*N + k)*v; special: (d-1)*N + temp*node; BOT3: ((n-1)*N + 8*node)*v
-    int32_t tab2;     // MF_BFG: the parent's table (f: posi*32, g: posi*64)
-    int32_t pad1;
+    int32_t tab2;     // MF_BFG: the parent's table (f: posi*32, g: posi*64); MF_FF: the child's f table
+    int32_t pad1;     // MF_FF: the child's S pointer field (4*(d+2))
 };
 
 struct FastPlan {
@@ -375,6 +386,48 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
     }
 }
 
+// f / g op with its left child's f folded in (MF_FF, fuse_descent in
+// qpd_capi.hip): SCLLUTDecoder.cpp:83-89 / :157-164 at depth d, then :83-89
+// at depth d+1.  Word u of S[d+2] is f(word u, word u + nwc) of S[d+1], both
+// produced by this lane, so the child's inputs come from registers instead of
+// a re-read of the row just stored (S[d+1] is still stored: the child's g
+// reads it later).  Chunks of two S[d+2] words per set; S[d] in the slab.
+template <bool ISG, int DL, int CDL, int NS>
+__device__ __forceinline__ void ff_op(const Mem (&M)[NS], const MOp &op, const int (&src)[NS], const int (&usrc)[NS],
+                                      uint32_t T, uint32_t T2, int lane) {
+    const int nwo = op.cnt >> 3, nwc = nwo >> 1;  // nwc even (op.cnt >= 32)
+    const bool ul = op.flags & MF_U_LDS;
+    for (int u0 = 0; u0 < nwc; u0 += 2) {
+        uint32_t A[NS][4], B[NS][4], ub[NS][2], X[NS][4];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int w = (k < 2 ? 0 : nwc) + u0 + (k & 1);
+                A[s][k] = M[s].ld(false, op.src_row + w, src[s]);
+                B[s][k] = M[s].ld(false, op.src_row + nwo + w, src[s]);
+            }
+            ub[s][0] = ub[s][1] = 0u;
+            if (ISG) {
+                ub[s][0] = M[s].ld(ul, op.u_row + (u0 >> 2), usrc[s]);
+                ub[s][1] = M[s].ld(ul, op.u_row + ((nwc + u0) >> 2), usrc[s]);
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int w = (k < 2 ? 0 : nwc) + u0 + (k & 1);
+                X[s][k] = lut_vec<8>(T, A[s][k], B[s][k], ub[s][k >> 1] >> ((w & 3) << 3));
+                M[s].st(DL != 0, op.dst_row + w, lane, X[s][k]);
+            }
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int k = 0; k < 2; ++k) M[s].st(CDL != 0, op.r_row + u0 + k, lane, lut_vec<8>(T2, X[s][k], X[s][k + 2], 0u));
+    }
+}
+
 // Bit i of b (i < 8) -> nibble i all ones.
 __device__ __forceinline__ uint32_t nib_mask(uint32_t b) {
     b &= 0xFFu;
@@ -444,6 +497,7 @@ __device__ __forceinline__ Pre fetch_pre(const FastPlan &P, const MOp &op, int l
     p.V = 0;
     if (op.type == OP_F || op.type == OP_LEAF_L) p.T = tab_ld(P.f_tab, op.tab * QPD_EXP_TABMUL, lane & 31);
     if ((op.type == OP_G && !(op.flags & MF_GSEL)) || op.type == OP_LEAF_R) p.T = tab_ld(P.g_tab, op.tab * QPD_EXP_TABMUL, lane);
+    if ((op.type == OP_F || op.type == OP_G) && (op.flags & MF_FF)) p.T2 = tab_ld(P.f_tab, op.tab2 * QPD_EXP_TABMUL, lane & 31);
     if (op.type == OP_BOT3) {
         p.T = tab_ld(P.f_tab, op.tab * QPD_EXP_TABMUL * 32, lane & 31);
         if (op.flags & MF_BFG)
@@ -542,6 +596,19 @@ __device__ __forceinline__ bool keep_all8(uint64_t K, uint64_t F, int gl) {
         if ((up & srt) == ~0ull) return true;
     }
 #endif
+#ifndef QPD_IDENT_MAX  // the group maximum by a 3-step DPP reduction (round 3): 1.1 % slower (r04q)
+    // With the keeps in order the largest is slot 7's, so no reduction: lanes
+    // 4-7 of each group take K_7 (quad broadcast) and the flips of slots 7-4
+    // (own) and 3-0 (half-row mirror) and compare both -- three independent
+    // lane moves instead of a dependent max chain.  (Unordered keeps fail the
+    // order ballot whatever K_7 is.)
+    const uint64_t k7 = dpp64<kDppQuadBcast3>(K);
+    const uint64_t fm = dpp64<kDppHalfMirror>(F);
+    const uint64_t Kn = dpp64<kDppRowShl1>(K);  // keep of slot gl+1
+    (void)gl;
+    const uint64_t up = (__builtin_amdgcn_ballot_w64(F >= k7) & __builtin_amdgcn_ballot_w64(fm >= k7)) | 0x0F0F0F0F0F0F0F0Full;
+    return (up & (__builtin_amdgcn_ballot_w64(K <= Kn) | 0x8080808080808080ull)) == ~0ull;
+#else
     uint64_t mk = K;
     mk = dmax_bits(mk, dpp64<kDppXor1>(mk));
     mk = dmax_bits(mk, dpp64<kDppXor2>(mk));
@@ -549,6 +616,7 @@ __device__ __forceinline__ bool keep_all8(uint64_t K, uint64_t F, int gl) {
     const uint64_t Kn = dpp64<kDppRowShl1>(K);       // keep of slot gl+1
     (void)gl;
     return (__builtin_amdgcn_ballot_w64(F >= mk) & (__builtin_amdgcn_ballot_w64(K <= Kn) | 0x8080808080808080ull)) == ~0ull;
+#endif
 }
 
 // Info leaf with quanta dm: keep the L best of {keep, flip} candidates.
@@ -773,6 +841,14 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
         uint32_t res = (c3l ^ c3r) | (c3r << 4);  // combine at depth n-3
         if (op.flags & MF_BCOMB)  // and the parent's (utils.cpp:62-67): U[n-3] of this lineage ^ res | res
             res = ((M[s].ld(op.flags & MF_U_LDS, op.u_row, gbase + pfield(st[s].U(), op.sh_u)) & 0xFFu) ^ res) | (res << 8);
+        if (op.flags & MF_BC2) {  // and the grandparent's: U[n-4] ^ res | res, 32 bits
+            const int e = op.pad1;
+            res = ((M[s].ld(op.flags & MF_BC2_ULDS, op.r_row, gbase + pfield(st[s].U(), e & 255)) & 0xFFFFu) ^ res) |
+                  (res << 16);
+            M[s].st(op.flags & MF_BC2_DLDS, e >> 16, lane, res);
+            if (!(op.flags & MF_BC2_TOR)) st[s].U() = pset(st[s].U(), (e >> 8) & 255, gl);
+            continue;
+        }
         M[s].st(op.flags & MF_DST_LDS, op.dst_row, lane, res);
         if (!(op.flags & MF_TO_R)) st[s].U() = pset(st[s].U(), op.sh_dst, gl);
     }
@@ -1299,6 +1375,25 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                         src[s] = gbase + pfield(stv[s].ps, op.sh_src);
                         usrc[s] = gbase + pfield(stv[s].U(), op.sh_u);
                     }
+                    if constexpr (KIND == K_SCL_LUT && NS >= 2) {
+                        if (fl & MF_FF) {  // + the left child's f (fuse_descent)
+                            const int key = ((fl & MF_DST_LDS) ? 1 : 0) | ((fl & MF_FF_DL) ? 2 : 0);
+#define QPD_FF(G, D_, C_) ff_op<G, D_, C_, NS>(Mv, op, src, usrc, cur.T, cur.T2, lane)
+                            if (op.type == OP_F) {
+                                if (key == 0) QPD_FF(false, 0, 0);
+                                else if (key == 2) QPD_FF(false, 0, 1);
+                                else QPD_FF(false, 1, 1);
+                            } else {
+                                if (key == 0) QPD_FF(true, 0, 0);
+                                else if (key == 2) QPD_FF(true, 0, 1);
+                                else QPD_FF(true, 1, 1);
+                            }
+#undef QPD_FF
+#pragma unroll
+                            for (int s = 0; s < NS; ++s) stv[s].ps = pset(pset(stv[s].ps, op.sh_dst, gl), op.pad1, gl);
+                            break;
+                        }
+                    }
                     if (fl & MF_GSEL)
                         gsel_op(Mv, op, yv, usrc, lane);
                     else if (NS >= 2 && !(fl & (MF_CHAN | MF_PRE))) {  // (one-set FastSCL: smaller code measured faster)
@@ -1419,7 +1514,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                             if (fl & MF_PM) {
                                 const uint64_t b = (uint64_t)src[op.src_row << 6] | ((uint64_t)src[(op.src_row + 1) << 6] << 32);
                                 stv[s].pm = gl < live ? __builtin_bit_cast(double, b) : kInf;
-                            } else {  // live rows into every path's own column
+                                            } else {  // live rows into every path's own column
                                 for (int w = 0; w < op.cnt; ++w) Mv[s].st(dl, op.dst_row + w, lane, src[(op.src_row + w) << 6]);
                             }
                         }
