@@ -70,6 +70,7 @@ struct qpd_decoder {
     int64_t scratch_bytes_per_wave;
     int engine = QPD_ENGINE_GENERIC;
     int lds_bytes = 0;
+    int lds_tab_bytes = 0;  // of lds_bytes: the f / g ops' byte tables (SCL-LUT)
     int pub_kind = 0;  // the kind the caller asked for (CRC-aided kinds map to their list kind)
     int out_bits = 0;  // bits per decoded frame: K, or A for the CRC-aided kinds
     int ca_A = 0, crc_n = 0;
@@ -1133,7 +1134,10 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     }
     F.lds_rows = rl;
     F.glb_rows = std::max(rg, 1);
-    d->lds_bytes = NS * (qpd::kSelInts * 4 + rl * 256);
+    // + SCL-LUT's byte tables of the f / g ops (stage_tab in qpd_fast.hip: 512 B for the
+    // op's table, 256 B for a folded child's f), after the sets' selection scratch
+    d->lds_tab_bytes = c->kind == QPD_SCL_LUT ? 768 : 0;
+    d->lds_bytes = NS * (qpd::kSelInts * 4 + rl * 256) + d->lds_tab_bytes;
     std::vector<qpd::MOp> mops;
     std::vector<uint16_t> r1tab;
     d->pre = Ly.pre;
@@ -1642,7 +1646,7 @@ int fast_launch(qpd_decoder *d, qpd::FastPlan fp, const int32_t *in, int64_t Bc,
     fp.task_base = d->task_base;
     void *args[] = {&fp, &in, &Bc, &out, &ops_arg};
     // the prefix stages run pfx_sets frame sets per wave in the same per-set layout
-    const size_t lds = (size_t)(d->lds_bytes / d->sets * sets);
+    const size_t lds = (size_t)((d->lds_bytes - d->lds_tab_bytes) / d->sets * sets + d->lds_tab_bytes);
     const int rc = timed_launch(d, prefix ? QPD_KC_PFX : QPD_KC_DECODE, st, [&]() -> int {
         QPD_HIP(hipLaunchKernel(kfn, dim3(fgrid), dim3(64), args, lds, st));
         QPD_HIP(hipGetLastError());

@@ -293,6 +293,51 @@ __device__ __forceinline__ uint32_t lut_vec(uint32_t T, uint32_t A, uint32_t B, 
     return out;
 }
 
+// The same NE lookups from the op's table staged as bytes in LDS (SCL-LUT's
+// f / g ops: stage_tab, then lut_lds): entry i of the f table (256) or of the
+// g table (512: u = 0, then u = 1) at byte i, read by ds_read_u8.  The address
+// of element k is byte j = k/2 of X / Y (one v_bfe; for g, v_perm_b32 puts the
+// u bit above it), and the result is the nibble itself: two VALU per lookup
+// against about five for the bpermute form, whose address and nibble offset
+// need a shift each and the result a field extract.  The f table's 64 dwords
+// sit one per LDS bank (conflict-free); the g table's two halves share banks.
+__device__ __forceinline__ uint32_t nib2byte4(uint32_t x) {  // nibbles 0-3 of x -> bytes 0-3
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    return (x | (x << 4)) & 0x0F0F0F0Fu;
+}
+
+// Table dword `dw` (8 entries: f lanes & 31, g all 64 lanes) as 8 bytes at tb + 8 * dw.
+__device__ __forceinline__ void stage_tab(uint8_t *tb, uint32_t T, int dw) {
+    uint2 b;
+    b.x = nib2byte4(T & 0xFFFFu);
+    b.y = nib2byte4(T >> 16);
+    *(uint2 *)(tb + 8 * dw) = b;
+}
+
+template <int NE, bool ISG>
+__device__ __forceinline__ uint32_t lut_lds(const uint8_t *tb, uint32_t A, uint32_t B, uint32_t hi) {
+    const uint32_t X = ((A << 4) & 0xF0F0F0F0u) | (B & 0x0F0F0F0Fu);
+    const uint32_t Y = (A & 0xF0F0F0F0u) | ((B >> 4) & 0x0F0F0F0Fu);
+    uint32_t hx = 0, hy = 0;  // byte j = bit 2j / 2j+1 of hi (g: the u half)
+    if constexpr (ISG) {
+        hx = (((hi & 0x55u) * 0x02082080u) >> 7) & 0x01010101u;
+        hy = ((((hi >> 1) & 0x55u) * 0x02082080u) >> 7) & 0x01010101u;
+    }
+    uint32_t out = 0;
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+        const int j = k >> 1;
+        const uint32_t W = (k & 1) ? Y : X;
+        uint32_t idx;
+        if constexpr (ISG)  // byte 0 = byte j of W, byte 1 = byte j of the u bits, bytes 2-3 = 0
+            idx = __builtin_amdgcn_perm((k & 1) ? hy : hx, W, (uint32_t)(j | ((4 + j) << 8) | (0x0C << 16) | (0x0C << 24)));
+        else
+            idx = __builtin_amdgcn_ubfe(W, 8 * j, 8);
+        out |= (uint32_t)tb[idx] << (4 * k);
+    }
+    return out;
+}
+
 // f / g op (SCLLUTDecoder.cpp:83-89 / :157-164): child symbols at depth d+1,
 // for each of the wave's NS frame sets.  Words are processed in chunks whose
 // loads are all issued before the first lookup: the shallow levels live in
@@ -308,9 +353,11 @@ __device__ __forceinline__ uint32_t fg_word(const FastPlan &P, const Mem &M, con
     return sym_word(P, M, op, y, src, w, cnt);
 }
 
-template <bool ISG, bool RAW, int NS, int SL = -1, int DL = -1>
+// LT: lookups from the byte table staged at tb (lut_lds) instead of T.
+template <bool ISG, bool RAW, int NS, int SL = -1, int DL = -1, bool LT = false>
 __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], const MOp &op, const int32_t *const (&y)[NS],
-                                      const int (&src)[NS], const int (&usrc)[NS], uint32_t T, int lane) {
+                                      const int (&src)[NS], const int (&usrc)[NS], uint32_t T, int lane,
+                                      const uint8_t *tb = nullptr) {
     const int ctemp = op.cnt;
     const bool dl = DL >= 0 ? DL != 0 : (op.flags & MF_DST_LDS) != 0, ul = op.flags & MF_U_LDS;
     if (ctemp >= 64) {
@@ -332,7 +379,9 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
                 for (int s = 0; s < NS; ++s)
 #pragma unroll
                     for (int k = 0; k < 4; ++k)
-                        M[s].st(dl, op.dst_row + w0 + k, lane, lut_vec<8>(T, A[s][k], B[s][k], ub[s] >> (k << 3)));
+                        M[s].st(dl, op.dst_row + w0 + k, lane,
+                                LT ? lut_lds<8, ISG>(tb, A[s][k], B[s][k], ub[s] >> (k << 3))
+                                   : lut_vec<8>(T, A[s][k], B[s][k], ub[s] >> (k << 3)));
             }
         } else {
             for (int w0 = 0; w0 < nwo; w0 += 8) {
@@ -370,7 +419,10 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
         for (int s = 0; s < NS; ++s)
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (k < nwo) M[s].st(dl, op.dst_row + k, lane, lut_vec<8>(T, A[s][k], B[s][k], ub[s] >> (k << 3)));
+                if (k < nwo)
+                    M[s].st(dl, op.dst_row + k, lane,
+                            LT ? lut_lds<8, ISG>(tb, A[s][k], B[s][k], ub[s] >> (k << 3))
+                               : lut_vec<8>(T, A[s][k], B[s][k], ub[s] >> (k << 3)));
     } else {  // ctemp in {2, 4}: the whole depth-d node (a then b) is one word
         uint32_t W[NS], ub[NS];
 #pragma unroll
@@ -392,9 +444,10 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
 // produced by this lane, so the child's inputs come from registers instead of
 // a re-read of the row just stored (S[d+1] is still stored: the child's g
 // reads it later).  Chunks of two S[d+2] words per set; S[d] in the slab.
+// The op's table is staged at tb, the child's f table at tb + 512 (lut_lds).
 template <bool ISG, int DL, int CDL, int NS>
 __device__ __forceinline__ void ff_op(const Mem (&M)[NS], const MOp &op, const int (&src)[NS], const int (&usrc)[NS],
-                                      uint32_t T, uint32_t T2, int lane) {
+                                      const uint8_t *tb, int lane) {
     const int nwo = op.cnt >> 3, nwc = nwo >> 1;  // nwc even (op.cnt >= 32)
     const bool ul = op.flags & MF_U_LDS;
     for (int u0 = 0; u0 < nwc; u0 += 2) {
@@ -418,13 +471,14 @@ __device__ __forceinline__ void ff_op(const Mem (&M)[NS], const MOp &op, const i
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int w = (k < 2 ? 0 : nwc) + u0 + (k & 1);
-                X[s][k] = lut_vec<8>(T, A[s][k], B[s][k], ub[s][k >> 1] >> ((w & 3) << 3));
+                X[s][k] = lut_lds<8, ISG>(tb, A[s][k], B[s][k], ub[s][k >> 1] >> ((w & 3) << 3));
                 M[s].st(DL != 0, op.dst_row + w, lane, X[s][k]);
             }
 #pragma unroll
         for (int s = 0; s < NS; ++s)
 #pragma unroll
-            for (int k = 0; k < 2; ++k) M[s].st(CDL != 0, op.r_row + u0 + k, lane, lut_vec<8>(T2, X[s][k], X[s][k + 2], 0u));
+            for (int k = 0; k < 2; ++k)
+                M[s].st(CDL != 0, op.r_row + u0 + k, lane, lut_lds<8, false>(tb + 512, X[s][k], X[s][k + 2], 0u));
     }
 }
 
@@ -1275,6 +1329,9 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
     // rows: set s's slots at sel_all + s * 64, its junk slots NS * 64 words on
     const int sstride = 64;
     int *const sel_all = (int *)(lds_dyn + NS * P.lds_rows * 64);
+    // SCL-LUT: the f / g ops' byte tables (stage_tab), 768 B after the selection scratch
+    constexpr bool kLdsTab = KIND == K_SCL_LUT && NS >= 2;
+    uint8_t *const tb = (uint8_t *)(sel_all + NS * kSelInts);
     Mem Mv[NS];
     {
         uint32_t *const slab = P.scratch + (size_t)blockIdx.x * NS * P.glb_rows * 64;
@@ -1378,7 +1435,9 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                     if constexpr (KIND == K_SCL_LUT && NS >= 2) {
                         if (fl & MF_FF) {  // + the left child's f (fuse_descent)
                             const int key = ((fl & MF_DST_LDS) ? 1 : 0) | ((fl & MF_FF_DL) ? 2 : 0);
-#define QPD_FF(G, D_, C_) ff_op<G, D_, C_, NS>(Mv, op, src, usrc, cur.T, cur.T2, lane)
+                            stage_tab(tb, cur.T, op.type == OP_F ? (lane & 31) : lane);
+                            stage_tab(tb + 512, cur.T2, lane & 31);
+#define QPD_FF(G, D_, C_) ff_op<G, D_, C_, NS>(Mv, op, src, usrc, tb, lane)
                             if (op.type == OP_F) {
                                 if (key == 0) QPD_FF(false, 0, 0);
                                 else if (key == 2) QPD_FF(false, 0, 1);
@@ -1399,7 +1458,9 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                     else if (NS >= 2 && !(fl & (MF_CHAN | MF_PRE))) {  // (one-set FastSCL: smaller code measured faster)
                         // row spaces of source and destination fixed per instantiation
                         const int key = ((fl & MF_SRC_LDS) ? 1 : 0) | ((fl & MF_DST_LDS) ? 2 : 0);
-#define QPD_FG(G, S_, D_) fg_op<G, true, NS, S_, D_>(P, Mv, op, yv, src, usrc, cur.T, lane)
+                        if constexpr (kLdsTab)
+                            if (op.cnt >= 8) stage_tab(tb, cur.T, op.type == OP_F ? (lane & 31) : lane);
+#define QPD_FG(G, S_, D_) fg_op<G, true, NS, S_, D_, kLdsTab>(P, Mv, op, yv, src, usrc, cur.T, lane, tb)
                         if (op.type == OP_F) {
                             if (key == 0) QPD_FG(false, 0, 0);
                             else if (key == 1) QPD_FG(false, 1, 0);
