@@ -801,10 +801,12 @@ __device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], u
 #ifndef QPD_BOT3_LAZY
 #define QPD_BOT3_LAZY 1
 #endif
-template <bool kList, bool L8, bool LAZY, int NS, class PF, class Path>
+// LT: the folded parent's lookups (MF_BFG) from its table staged as bytes at tb (lut_lds).
+template <bool kList, bool L8, bool LAZY, bool LT, int NS, class PF, class Path>
 __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], const MOp &op,
                                         const int32_t *const (&y)[NS], Path (&st)[NS], uint32_t Tf0, uint32_t T2, int gl,
-                                        int gbase, int L, int *sel, int sstride, int lane, PF &&prefetch_next) {
+                                        int gbase, int L, int *sel, int sstride, int lane, PF &&prefetch_next,
+                                        uint8_t *tb) {
     const int p0 = op.tab * QPD_EXP_TABMUL;
     const int fr = op.cnt;
     const uint32_t *ft = P.f_tab, *gt = P.g_tab;
@@ -837,12 +839,13 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
         // The depth n-4 parent's f / g (SCLLUTDecoder.cpp:83-89 / :157-164,
         // ctemp = 8) folded in: W3 from the parent's 16 symbols, in registers.
         const bool sl = op.flags & MF_SRC_LDS, ul = op.flags & MF_U_LDS;
+        if constexpr (LT) stage_tab(tb, T2, (op.flags & MF_BG) ? lane : (lane & 31));
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             const int src = gbase + pfield(st[s].ps, op.sh_src);
             const uint32_t a = M[s].ld(sl, op.src_row, src), b = M[s].ld(sl, op.src_row + 1, src);
             const uint32_t ub = (op.flags & MF_BG) ? M[s].ld(ul, op.u_row, gbase + pfield(st[s].U(), op.sh_u)) : 0u;
-            x[s][0] = lut_vec<8>(T2, a, b, ub);
+            x[s][0] = LT ? lut_lds<8, true>(tb, a, b, ub) : lut_vec<8>(T2, a, b, ub);  // (ub = 0 for f: entries < 256)
         }
     } else {
 #pragma unroll
@@ -1420,9 +1423,9 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
             const int fl = op.flags;
             switch (op.type) {
                 case OP_BOT3:
-                    bot3_op<kList, L8, kLazy>(P, Mv, op, yv, stv, cur.T, cur.T2, gl, gbase, L, sel_all, sstride, lane, [&]() {
+                    bot3_op<kList, L8, kLazy, kLdsTab>(P, Mv, op, yv, stv, cur.T, cur.T2, gl, gbase, L, sel_all, sstride, lane, [&]() {
                         if (oi + 1 < P.nops) pre = fetch_pre(P, nxt, lane, vlane);
-                    });
+                    }, tb);
                     break;
                 case OP_F:
                 case OP_G: {
@@ -1802,15 +1805,21 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
 // nibble selects (MF_GSEL, gsel_op).  Out-of-range symbols raise the error
 // flag here, as chan_word8 does in the decode kernel.
 // ---------------------------------------------------------------------------
+// The root's f and g tables as bytes in LDS once per block (stage_tab): an
+// element's 8-bit index addresses all three results (f, g with u = 0 at +0,
+// u = 1 at +256) -- one field extract and three ds_read_u8 per element.
 __global__ __launch_bounds__(256) void root_pre_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
                                                        uint32_t *__restrict__ pre) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t Tf = P.f_tab[lane & 31], Tg = P.g_tab[lane];  // node 0 (posi 0)
-    const int wsh = P.n - 4;                                      // log2 words per segment
+    __shared__ __attribute__((aligned(16))) uint8_t tf[256], tg[512];
+    if (threadIdx.x < 64) {  // node 0 (posi 0)
+        stage_tab(tg, P.g_tab[threadIdx.x], threadIdx.x);
+        if (threadIdx.x < 32) stage_tab(tf, P.f_tab[threadIdx.x], threadIdx.x);
+    }
+    __syncthreads();
+    const int wsh = P.n - 4;  // log2 words per segment
     const int half = P.N >> 1;
     const int64_t total = B << wsh;
     for (int64_t base = (int64_t)blockIdx.x * 256; base < total; base += (int64_t)gridDim.x * 256) {
-        // whole waves stay active through the ds_bpermute lookups (inactive lanes read as 0)
         const int64_t t0 = base + threadIdx.x;
         const int64_t t = t0 < total ? t0 : total - 1;
         const int64_t f = t >> wsh;
@@ -1818,9 +1827,16 @@ __global__ __launch_bounds__(256) void root_pre_kernel(FastPlan P, const int32_t
         const int32_t *y = in + (f << P.n);
         const uint32_t a = chan_word8(y, 8 * w, P.in_vec, P.v, P.err);
         const uint32_t b = chan_word8(y, half + 8 * w, P.in_vec, P.v, P.err);
-        const uint32_t fw = lut_vec<8>(Tf, a, b, 0u);
-        const uint32_t g0 = lut_vec<8>(Tg, a, b, 0u);
-        const uint32_t g1 = lut_vec<8>(Tg, a, b, 0xFFu);
+        const uint32_t X = ((a << 4) & 0xF0F0F0F0u) | (b & 0x0F0F0F0Fu);  // byte j: index of element 2j
+        const uint32_t Y = (a & 0xF0F0F0F0u) | ((b >> 4) & 0x0F0F0F0Fu);  // ... of element 2j + 1
+        uint32_t fw = 0, g0 = 0, g1 = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t idx = __builtin_amdgcn_ubfe((k & 1) ? Y : X, 8 * (k >> 1), 8);
+            fw |= (uint32_t)tf[idx] << (4 * k);
+            g0 |= (uint32_t)tg[idx] << (4 * k);
+            g1 |= (uint32_t)tg[256 + idx] << (4 * k);
+        }
         if (t0 < total) {
             uint32_t *row = pre + (f << (P.n - 2));
             row[w] = fw;
