@@ -18,12 +18,18 @@ def _sources():
     return [os.path.join(SRC, f) for f in sorted(os.listdir(SRC))] + [os.path.join(ROOT, "include", "qpd.h")]
 
 
-# Translation units and their own flags.  The FastSCL-LUT kernels take the
-# max-ILP machine scheduler (measured +5 % there, -0.5 % on SCL-LUT; see
-# qpd_fast_fscl.hip), so they are a separate unit.
+# Translation units and their own flags (compiled in parallel): the C-ABI (host
+# code, the pre-pass / Monte-Carlo / probe kernels), the decode kernel
+# instantiations of SC/SCL/FastSC-LUT and of FastSCL-LUT (one template,
+# qpd_fast.hip), the generic engine's, the LUT generator.
 UNITS = [
     ("qpd_capi.hip", []),
-    ("qpd_fast_fscl.hip", ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]),
+    ("qpd_k_fast.hip", []),
+    ("qpd_k_scl.hip", []),
+    ("qpd_k_scl1.hip", []),
+    ("qpd_fast_fscl.hip", []),
+    ("qpd_fast_fscl1.hip", []),
+    ("qpd_k_generic.hip", []),
     ("qpd_lutgen.cpp", []),
 ]
 COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
@@ -70,8 +76,10 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
     common = [HIPCC, f"--offload-arch={ARCH}"] + COMMON_FLAGS + ["-I", os.path.join(ROOT, "include"), "-I", SRC,
                                                                  f'-DQPD_BUILD_ID="{bid}"']
     objs, procs = [], []
+    odir = os.path.join(ROOT, "build", "obj")  # kept: tools/build_variant.sh links variants against them
+    os.makedirs(odir, exist_ok=True)
     for src, extra in UNITS:  # the units compile in parallel
-        obj = os.path.join(HERE, os.path.splitext(src)[0] + ".o")
+        obj = os.path.join(odir, os.path.splitext(src)[0] + ".o")
         cmd = common + extra + ["-c", os.path.join(SRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
@@ -84,8 +92,6 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    for o in objs:
-        os.remove(o)
     os.replace(LIB + ".tmp", LIB)
     return LIB
 

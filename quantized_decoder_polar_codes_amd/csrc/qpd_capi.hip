@@ -15,9 +15,18 @@
 #include "qpd_generic.hip"
 #include "qpd_fast.hip"
 
+// Kernel instantiations, each in its own translation unit (build.py UNITS:
+// the units compile in parallel).  Diagnostic builds that read device
+// globals (QPD_STAMPS) compile them into this unit instead (the end of the file).
 namespace qpd {
-const void *fast_kernel_fscl(int sets, bool l8, bool r1l);  // qpd_fast_fscl.hip
-}
+const void *fast_kernel_single(int kind, int sets);              // qpd_k_fast.hip
+const void *prefix_kernel(int kind, int sets, bool pw1);         // qpd_k_fast.hip
+const void *fast_kernel_scl(int sets, bool l8);                  // qpd_k_scl.hip
+const void *fast_kernel_scl_pw1(int sets, bool l8);              // qpd_k_scl1.hip
+const void *fast_kernel_fscl(int sets, bool l8, bool r1l);       // qpd_fast_fscl.hip
+const void *fast_kernel_fscl_pw1(int sets, bool l8, bool r1l);   // qpd_fast_fscl1.hip
+const void *generic_kernel(int fam, int dom, bool wide);         // qpd_k_generic.hip
+}  // namespace qpd
 #include "qpd_mc.hip"
 #include "qpd_probe.hip"
 #include "qpd_host.hpp"
@@ -314,6 +323,8 @@ struct FastLayout {
     int lds_end = 0;                        // rows incl. the selection scratch
     bool pre = false;    // root pre-pass (root_pre_kernel): MF_PRE / MF_GSEL ops at the root
     bool bfuse = false;  // BOT3 children of depth n-4 nodes fold in the parent's F / G / COMB
+    int ns = 1;          // frame sets per wave (their rows interleave)
+    bool botx = false;   // FastSCL-LUT, L = 8: height-3 subtrees with special nodes as BOT3 ops (MF_BOTX)
     bool lds(int dd) const { return dd >= D; }
 };
 
@@ -324,6 +335,56 @@ bool bot3_plain(int kind, const int32_t *node_type, int n, int d, int node) {
         for (int k = 0; k < (1 << (dd - d)); ++k)
             if (special_of(kind, node_type, (1 << dd) + (node << (dd - d)) + k - 1) >= 0) return false;
     return true;
+}
+
+// The elements of the special node (d, node) share one quanta row vcl[d-1][pos]
+// (MF_VUNI's condition; every MinDistortion table qualifies).
+bool quanta_uniform(const double *vcl, int N, int v, int d, int node) {
+    const int temp = N >> d;
+    const uint64_t *q = (const uint64_t *)(vcl + ((size_t)(d - 1) * N + (size_t)temp * node) * v);
+    for (int j = 1; j < temp; ++j)
+        if (std::memcmp(q, q + (size_t)j * v, sizeof(double) * v) != 0) return false;
+    return true;
+}
+
+// A height-3 subtree under (d = n-3, node) that botx_op (qpd_fast.hip) can run in
+// registers: its nodes of size 4 and 2 plain or FastSCL special nodes (R0 / R1 /
+// REP) with one quanta row each.  *ty = the types, two bits per node (q1, q2,
+// then q3..q6; BX_* in qpd_fast.hip).
+bool bot3_mixed(int kind, const int32_t *node_type, const double *vcl, int N, int n, int v, int node, int *ty) {
+    if (kind != QPD_FASTSCL_LUT || n < 4 || v > 16) return false;
+    const int d = n - 3;
+    if (special_of(kind, node_type, (1 << d) + node - 1) >= 0) return false;
+    int t = 0;
+    bool any = false;
+    for (int h = 0; h < 2; ++h) {
+        const int q = 2 * node + h;  // size-4 node at depth n-2
+        const int s4 = special_of(kind, node_type, (1 << (d + 1)) + q - 1);
+        if (s4 >= 0) {
+            if (!quanta_uniform(vcl, N, v, d + 1, q)) return false;
+            t |= (1 + s4) << (2 * h);  // R0 / R1 / REP = 0 / 1 / 2 -> BX_R0 / BX_R1 / BX_REP
+            any = true;
+            continue;
+        }
+        for (int c = 0; c < 2; ++c) {
+            const int k = 2 * h + c, q2 = 2 * q + c;  // size-2 node at depth n-1
+            const int s2 = special_of(kind, node_type, (1 << (d + 2)) + q2 - 1);
+            if (s2 < 0) continue;
+            if (!quanta_uniform(vcl, N, v, d + 2, q2)) return false;
+            t |= (1 + s2) << (4 + 2 * k);
+            any = true;
+        }
+    }
+    // diagnosis: QPD_BOTX_SEL = allowed types (bit 1 R0, 2 R1, 3 REP) | size-4 (bit 4) / size-2 (bit 5)
+    if (const char *e = getenv("QPD_BOTX_SEL")) {
+        const int sel = atoi(e);
+        for (int i = 0; i < 6; ++i) {
+            const int x = (t >> (2 * i)) & 3;
+            if (x && (!(sel & (1 << x)) || !(sel & (i < 2 ? 16 : 32)))) return false;
+        }
+    }
+    *ty = t;
+    return any;
 }
 
 // R1 argsort keys of the fast engine (FastSCL, node size <= 32): for element j
@@ -386,8 +447,9 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
             m.tab = (int)r1tab.size();  // rank-key table of this node
             r1_rank_table(r1tab, vcl, N, v, d, node);
             // > 16 elements: std::sort's introsort runs on 16-bit entries in the
-            // free LDS tail (rows of depths > d + the selection scratch)
-            if (m.cnt > qpd::stl::kThreshold && Ly.lds(d + 1) && Ly.lds_end - Ly.lds_base[d + 1] >= m.cnt / 2) {
+            // free LDS tail of the wave (the sets' rows of depths > d + their
+            // selection scratch; build_fast pads the LDS rows to make room)
+            if (m.cnt > qpd::stl::kThreshold && Ly.lds(d + 1) && Ly.ns * (Ly.lds_end - Ly.lds_base[d + 1]) >= m.cnt / 2) {
                 m.flags |= MF_R1_LDS;
                 m.u_row = Ly.lds_base[d + 1];
             }
@@ -396,10 +458,16 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
         out.push_back(m);
         return;
     }
+    int bx_ty = 0;
     if (n >= 3 && d == n - 3) {
-        if (bot3_plain(kind, node_type, n, d, node)) {
+        const bool mixed = Ly.botx && bot3_mixed(kind, node_type, vcl, N, n, v, node, &bx_ty);
+        if (mixed || bot3_plain(kind, node_type, n, d, node)) {
             MOp m = base(OP_BOT3);
             for (int j = 0; j < 8; ++j) m.cnt |= (frozen[8 * node + j] == 1) << j;
+            if (mixed) {
+                m.flags |= MF_BOTX;
+                m.cnt |= bx_ty << 8;
+            }
             m.tab = posi;
             m.vrow = ((n - 1) * N + 8 * node) * v;
             finish_node(m);
@@ -411,8 +479,12 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
         // Both children plain BOT3 subtrees of a depth n-4 node (d >= 2: S[d] is
         // a slab/LDS row): the left BOT3 takes this node's f, the right one its g
         // and then this node's combine -- no F / G / COMB ops, no S[n-3] rows.
-        const bool fuse = Ly.bfuse && d == n - 4 && d >= 2 && bot3_plain(kind, node_type, n, d + 1, 2 * node) &&
-                          bot3_plain(kind, node_type, n, d + 1, 2 * node + 1);
+        int t0 = 0;
+        auto bot3_able = [&](int c) {  // the child (d + 1, c) becomes a BOT3 op
+            return bot3_plain(kind, node_type, n, d + 1, c) ||
+                   (Ly.botx && bot3_mixed(kind, node_type, vcl, N, n, v, c, &t0));
+        };
+        const bool fuse = Ly.bfuse && d == n - 4 && d >= 2 && bot3_able(2 * node) && bot3_able(2 * node + 1);
         for (int side = 0; side < 2; ++side) {
             MOp m = base(side ? OP_G : OP_F);
             m.cnt = N >> (d + 1);
@@ -866,56 +938,19 @@ int ensure_records(DeviceBuf &b, size_t &cap, int64_t Bc, int rec, int paths) {
 #endif
 constexpr int kDefaultSets = QPD_DEFAULT_SETS;
 
-// Instantiations of lut_fast_kernel<KIND, NS, L8, R1L, PFX, PW1>; pw1: the
-// op list's pointer fields fit one word (compact_pointer_fields; SCL-LUT only).
+// The decode kernel instantiation of a plan (nullptr: none, the launch fails).
+// pw1: the op list's pointer fields fit one word (compact_pointer_fields).
 const void *fast_kernel(int kind, int sets, bool l8, bool r1l, bool pw1) {
-    using namespace qpd;
-    if (kind == QPD_SCL_LUT && pw1) {
-        if (sets == 2) return l8 ? reinterpret_cast<const void *>(&lut_fast_kernel<K_SCL_LUT, 2, true, false, false, true>)
-                                 : reinterpret_cast<const void *>(&lut_fast_kernel<K_SCL_LUT, 2, false, false, false, true>);
-        return l8 ? reinterpret_cast<const void *>(&lut_fast_kernel<K_SCL_LUT, 1, true, false, false, true>)
-                  : reinterpret_cast<const void *>(&lut_fast_kernel<K_SCL_LUT, 1, false, false, false, true>);
-    }
-#define QPD_FK(K, S, E) reinterpret_cast<const void *>(&lut_fast_kernel<K, S, E>)
-#define QPD_FKR(S, E) reinterpret_cast<const void *>(&lut_fast_kernel<K_FASTSCL_LUT, S, E, true>)
     switch (kind) {
-        case QPD_SC_LUT: return sets == 2 ? QPD_FK(K_SC_LUT, 2, false) : QPD_FK(K_SC_LUT, 1, false);
-        case QPD_FASTSC_LUT: return sets == 2 ? QPD_FK(K_FASTSC_LUT, 2, false) : QPD_FK(K_FASTSC_LUT, 1, false);
-        case QPD_SCL_LUT:
-#ifdef QPD_SETS3
-            if (sets == 3 && l8) return QPD_FK(K_SCL_LUT, 3, true);
-#endif
-            if (sets == 2) return l8 ? QPD_FK(K_SCL_LUT, 2, true) : QPD_FK(K_SCL_LUT, 2, false);
-            return l8 ? QPD_FK(K_SCL_LUT, 1, true) : QPD_FK(K_SCL_LUT, 1, false);
-        case QPD_FASTSCL_LUT:
-#ifndef QPD_STAMPS
-            return fast_kernel_fscl(sets, l8, r1l);  // qpd_fast_fscl.hip (own scheduler flags)
-#else
-            if (r1l) {
-                if (sets == 2) return l8 ? QPD_FKR(2, true) : QPD_FKR(2, false);
-                return l8 ? QPD_FKR(1, true) : QPD_FKR(1, false);
-            }
-            if (sets == 2) return l8 ? QPD_FK(K_FASTSCL_LUT, 2, true) : QPD_FK(K_FASTSCL_LUT, 2, false);
-            return l8 ? QPD_FK(K_FASTSCL_LUT, 1, true) : QPD_FK(K_FASTSCL_LUT, 1, false);
-#endif
-        default: return nullptr;
-    }
-#undef QPD_FKR
-#undef QPD_FK
-}
-
-const void *prefix_kernel(int kind, int sets, bool pw1) {
-    using namespace qpd;
-    switch (kind) {
-        case QPD_SCL_LUT:
-            if (pw1)
-                return sets == 2 ? reinterpret_cast<const void *>(&lut_prefix_kernel(K_SCL_LUT, 2, true))
-                                 : reinterpret_cast<const void *>(&lut_prefix_kernel(K_SCL_LUT, 1, true));
-            return sets == 2 ? reinterpret_cast<const void *>(&lut_prefix_kernel(K_SCL_LUT, 2, false))
-                             : reinterpret_cast<const void *>(&lut_prefix_kernel(K_SCL_LUT, 1, false));
+        case QPD_SC_LUT:
+        case QPD_FASTSC_LUT: return pw1 || r1l ? nullptr : qpd::fast_kernel_single(kind, sets);
+        case QPD_SCL_LUT: return r1l ? nullptr : pw1 ? qpd::fast_kernel_scl_pw1(sets, l8) : qpd::fast_kernel_scl(sets, l8);
+        case QPD_FASTSCL_LUT: return pw1 ? qpd::fast_kernel_fscl_pw1(sets, l8, r1l) : qpd::fast_kernel_fscl(sets, l8, r1l);
         default: return nullptr;
     }
 }
+using qpd::generic_kernel;
+using qpd::prefix_kernel;
 
 // One pointer word per path (PathT<true>, qpd_fast.hip): the S-row and U-row
 // pointer fields the op lists read or set, by op type (the access pattern of
@@ -1065,10 +1100,10 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
         L.lds_base[n + 1] = rl;
         L.lds_end = rl + qpd::kSelInts / 64;
     };
-    // one frame set for the Fast kinds: their special nodes' state spills at NS = 2
-    // (FastSCL's R1 argsort; FastSC-LUT N=1024: 171 -> 241 M frames/s with one set,
-    // profiles/r03z_sets.txt)
-    d->sets = (c->kind == QPD_FASTSCL_LUT || c->kind == QPD_FASTSC_LUT) ? 1 : kDefaultSets;
+    // one frame set for FastSC-LUT (N=1024: 171 -> 241 M frames/s with one set,
+    // profiles/r03z_sets.txt); two for the list kinds, FastSCL-LUT included (round 5:
+    // the SCL-LUT kernel's two-set machinery with the special-node ops)
+    d->sets = c->kind == QPD_FASTSC_LUT ? 1 : kDefaultSets;
     if (const char *e = getenv("QPD_SETS")) d->sets = std::min(2, std::max(1, atoi(e)));
 #ifdef QPD_SETS3
     if (const char *e = getenv("QPD_SETS")) if (atoi(e) == 3 && c->kind == QPD_SCL_LUT && d->L == 8) d->sets = 3;
@@ -1076,14 +1111,16 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     d->l8 = (c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT) && d->L == 8;
     const int NS = d->sets;
     FastLayout Ly;
+    Ly.ns = NS;
     const int32_t *nt_fast = (c->kind == QPD_FASTSC_LUT || c->kind == QPD_FASTSCL_LUT) ? c->node_type : nullptr;
     // pre-mode: S[1] is whole words (N >= 16) and the root's left child a plain node
     Ly.pre = n >= 4 && special_of(c->kind, nt_fast, 1) < 0 && !getenv("QPD_NO_PRE");
     Ly.bfuse = !getenv("QPD_NO_BFUSE");
-    // Trimmed layout, except where FastSCL's R1 argsorts (> 16 elements) use
-    // the LDS rows of the deeper levels as scratch: probe the op list on an
-    // all-global layout and keep the slots it touches.
-    if (!(c->kind == QPD_FASTSCL_LUT && s.max_r1 > qpd::stl::kThreshold) && !getenv("QPD_NO_TRIM")) {
+    Ly.botx = c->kind == QPD_FASTSCL_LUT && d->l8 && !getenv("QPD_NO_BOTX");
+    // Trimmed layout: probe the op list on an all-global layout and keep the
+    // slots it touches.  (FastSCL's R1 argsorts of > 16 elements borrow the LDS
+    // tail of the deeper levels; it is padded below where it is too short.)
+    if (!getenv("QPD_NO_TRIM")) {
         FastLayout Lp = Ly;
         Lp.D = n + 1;
         int pl = 0, pg = 0;
@@ -1113,14 +1150,33 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
         used[0][0] = true;  // R[0]: the tail re-encodes it
         std::memcpy(use, used, sizeof(use));
     }
-    // LDS per wave = NS * (selection scratch + rows of depths >= D); the budget
-    // is measured: occupancy beats LDS residency of the shallow depths.
+    // the list kinds' byte tables of the f / g ops at two frame sets (stage_tab in
+    // qpd_fast.hip: 512 B for the op's table, 256 B for a folded child's f), after the
+    // sets' selection scratch
+    const bool list_kind = c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT;
+    d->lds_tab_bytes = list_kind && NS >= 2 ? 768 : 0;
+    // LDS per wave = NS * (selection scratch + rows of depths >= D) + the byte
+    // tables; the budget is measured: occupancy beats LDS residency of the
+    // shallow depths.
     int budget = NS == 1 ? 6 * 1024 : NS == 2 ? 10 * 1024 : 15 * 1024;
     if (const char *e = getenv("QPD_LDS_BUDGET")) budget = atoi(e);
-    while (Ly.D <= n && NS * (qpd::kSelInts * 4 + lds_rows(Ly.D) * 256) > budget) ++Ly.D;
+    while (Ly.D <= n && NS * (qpd::kSelInts * 4 + lds_rows(Ly.D) * 256) + d->lds_tab_bytes > budget) ++Ly.D;
     F.lds_from = Ly.D;
     int rl = 0, rg = 0;
     assign(Ly, rl, rg);
+    // FastSCL R1 nodes of 17..32 elements sort in the wave's LDS tail of the
+    // deeper levels (MF_R1_LDS): pad the rows so that the tail holds cnt / 2 rows
+    {
+        int pad = 0;
+        for (const qpd::Op &o : s.ops)
+            if (c->kind == QPD_FASTSCL_LUT && o.type == qpd::OP_R1 && (N >> o.d) > qpd::stl::kThreshold &&
+                (N >> o.d) <= 32 && Ly.lds(o.d + 1)) {
+                const int have = NS * (Ly.lds_end - Ly.lds_base[o.d + 1]), need = (N >> o.d) / 2;
+                if (have < need) pad = std::max(pad, (need - have + NS - 1) / NS);
+            }
+        rl += pad;
+        Ly.lds_end += pad;
+    }
     F.R0_row = Ly.R[0];
     F.R0_lds = Ly.lds(0);
     F.H_row = F.K_row = F.I_row = rg;
@@ -1134,9 +1190,6 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     }
     F.lds_rows = rl;
     F.glb_rows = std::max(rg, 1);
-    // + SCL-LUT's byte tables of the f / g ops (stage_tab in qpd_fast.hip: 512 B for the
-    // op's table, 256 B for a folded child's f), after the sets' selection scratch
-    d->lds_tab_bytes = c->kind == QPD_SCL_LUT ? 768 : 0;
     d->lds_bytes = NS * (qpd::kSelInts * 4 + rl * 256) + d->lds_tab_bytes;
     std::vector<qpd::MOp> mops;
     std::vector<uint16_t> r1tab;
@@ -1181,15 +1234,15 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     // prefix_kernel() instantiates NS = 1 and 2 only: fast_launch's task count
     // (fgroups) must use the NS the launched kernel has
     if (const char *e = getenv("QPD_PFX_SETS")) d->pfx_sets = std::min(std::min(d->sets, 2), std::max(1, atoi(e)));
-    // folded descents: the SCL-LUT kernels with two frame sets (ff_op)
-    if (c->kind == QPD_SCL_LUT && !getenv("QPD_NO_FF")) {
+    // folded descents: the list kernels with two frame sets (ff_op)
+    if (list_kind && !getenv("QPD_NO_FF")) {
         if (d->sets == 2) fuse_descent(mops);
         if (d->pfx_sets == 2) {
             fuse_descent(pp.st1);
             fuse_descent(pp.st2);
         }
     }
-    if (c->kind == QPD_SCL_LUT && !getenv("QPD_NO_BC2")) {  // folded depth n-5 combines (any NS)
+    if (list_kind && !getenv("QPD_NO_BC2")) {  // folded depth n-5 combines (any NS)
         fold_combine(mops);
         fold_combine(pp.st1);
         fold_combine(pp.st2);
@@ -1197,7 +1250,13 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     place_syncs(pp.st1, true);
     place_syncs(pp.st2, true);
     place_syncs(mops, c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT);
-    if (c->kind == QPD_SCL_LUT && !getenv("QPD_NO_PW1")) d->pw1 = compact_pointer_fields({&mops, &pp.st1, &pp.st2});
+    // one pointer word: the list kinds at one or two frame sets (the instantiations
+    // fast_kernel() has); FastSCL-LUT only at two sets with L = 8 and no r1_large
+    for (const qpd::MOp &m : mops)  // R1 nodes the register/LDS argsort cannot take (r1_large)
+        if (c->kind == QPD_FASTSCL_LUT && m.type == qpd::OP_R1 && m.cnt > qpd::stl::kThreshold && !(m.flags & qpd::MF_R1_LDS))
+            d->r1l = true;
+    const bool pw1_ok = c->kind == QPD_SCL_LUT ? NS <= 2 : (c->kind == QPD_FASTSCL_LUT && NS == 2 && d->l8 && !d->r1l);
+    if (pw1_ok && !getenv("QPD_NO_PW1")) d->pw1 = compact_pointer_fields({&mops, &pp.st1, &pp.st2});
     d->pfx_nops = (int)pp.st1.size();
     d->pfx2_nops = (int)pp.st2.size();
     d->pfx1_rec = pp.rec1;
@@ -1211,9 +1270,6 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
         if (rc) return rc;
         d->main_ops_host = mops;  // the import ops get the record buffers' addresses (patch_imports)
     }
-    for (const qpd::MOp &m : mops)  // R1 nodes the register/LDS argsort cannot take
-        if (c->kind == QPD_FASTSCL_LUT && m.type == qpd::OP_R1 && m.cnt > qpd::stl::kThreshold && !(m.flags & qpd::MF_R1_LDS))
-            d->r1l = true;
     F.nops = (int)mops.size();
     d->num_mops = F.nops + d->pfx_nops + d->pfx2_nops;
     {
@@ -1270,43 +1326,6 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     return QPD_OK;
 }
 
-// Generic-engine instantiations generic_decode_kernel<family, domain>: every
-// family in the LUT and plain float domains; the re-quantized domains exist
-// only for SC and SCL (SC{,L}{Uniform,Lloyd}QuantizedDecoder).
-const void *generic_kernel(int fam, int dom, bool wide) {
-    using namespace qpd;
-#define QPD_GK(K, D) (wide ? reinterpret_cast<const void *>(&generic_decode_kernel<K, D, kMaxLWide>) \
-                           : reinterpret_cast<const void *>(&generic_decode_kernel<K, D, kMaxL>))
-#define QPD_GN(K, D) reinterpret_cast<const void *>(&generic_decode_kernel<K, D, kMaxL>)
-    // single-path families never need the wide list instantiation
-    switch (dom) {
-        case DOM_LUT:
-            switch (fam) {
-                case QPD_SC_LUT: return QPD_GN(K_SC_LUT, DOM_LUT);
-                case QPD_SCL_LUT: return QPD_GK(K_SCL_LUT, DOM_LUT);
-                case QPD_FASTSC_LUT: return QPD_GN(K_FASTSC_LUT, DOM_LUT);
-                case QPD_FASTSCL_LUT: return QPD_GK(K_FASTSCL_LUT, DOM_LUT);
-                default: return nullptr;
-            }
-        case DOM_FLOAT:
-            switch (fam) {
-                case QPD_SC_LUT: return QPD_GN(K_SC_LUT, DOM_FLOAT);
-                case QPD_SCL_LUT: return QPD_GK(K_SCL_LUT, DOM_FLOAT);
-                case QPD_FASTSC_LUT: return QPD_GN(K_FASTSC_LUT, DOM_FLOAT);
-                case QPD_FASTSCL_LUT: return QPD_GK(K_FASTSCL_LUT, DOM_FLOAT);
-                default: return nullptr;
-            }
-        case DOM_UNIFORM:
-            return fam == QPD_SC_LUT ? QPD_GN(K_SC_LUT, DOM_UNIFORM)
-                                     : fam == QPD_SCL_LUT ? QPD_GK(K_SCL_LUT, DOM_UNIFORM) : nullptr;
-        case DOM_LLOYD:
-            return fam == QPD_SC_LUT ? QPD_GN(K_SC_LUT, DOM_LLOYD)
-                                     : fam == QPD_SCL_LUT ? QPD_GK(K_SCL_LUT, DOM_LLOYD) : nullptr;
-        default: return nullptr;
-    }
-#undef QPD_GN
-#undef QPD_GK
-}
 
 template <class In>
 int launch_generic(qpd_decoder *d, const In *in, int64_t B, uint8_t *out, int grid, hipStream_t st) {
@@ -2140,3 +2159,13 @@ int qpd_debug_stamps(unsigned long long *out64) {
 }
 #endif
 }  // extern "C"
+
+#ifdef QPD_STAMPS  // (see the declarations at the top)
+#define QPD_UNIT_INCLUDED
+#include "qpd_k_fast.hip"
+#include "qpd_k_scl.hip"
+#include "qpd_k_scl1.hip"
+#include "qpd_fast_fscl.hip"
+#include "qpd_fast_fscl1.hip"
+#include "qpd_k_generic.hip"
+#endif

@@ -67,6 +67,7 @@ enum MopFlag : int32_t {
     MF_BC2_ULDS = 4194304,  //   ... that U row in LDS
     MF_BC2_DLDS = 8388608,  //   ... the result row in LDS
     MF_BC2_TOR = 16777216,  //   ... the grandparent is a right child (R row: no pointer update)
+    MF_BOTX = 33554432,     // BOT3 of a subtree with FastSCL special nodes of size 4 / 2 (botx_op)
 };
 
 struct MOp {
@@ -127,6 +128,10 @@ struct FastPlan {
 #endif
 #ifndef QPD_EXP_SLABMUL
 #define QPD_EXP_SLABMUL 1
+#endif
+
+#ifndef QPD_EXP_NO_BOTX
+#define QPD_EXP_NO_BOTX 0  // register-allocation experiments: botx_op compiled out (MF_BOTX ops then wrong)
 #endif
 
 #ifndef QPD_SLAB_AUX
@@ -912,6 +917,223 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
 }
 
 // ---------------------------------------------------------------------------
+// BOTX (FastSCL-LUT, L = 8; MF_BOTX): a height-3 subtree whose nodes of size
+// 4 or 2 include FastSCL special nodes (FastSCLLUTDecoder.cpp:83-213: R0, R1,
+// REP), held in registers like BOT3.  The types ride in op.cnt bits 8-19, two
+// bits per node: q1, q2 (size 4), then q3..q6 (size 2); 0 = plain (a size-4
+// node of two size-2 children / a leaf pair), else BX_R0 / BX_R1 / BX_REP
+// (nodes inside a special one: don't care).  Every special node's elements
+// share one quanta row (MF_VUNI's condition, checked by the host), which sits
+// in lanes 0-15 of the slot's quanta register.  The subtree runs as four leaf
+// slots (the pairs under q3..q6), a loop that is not unrolled, each slot
+// loading its own tables and quanta: a size-4 special node takes its half's
+// first slot and skips the second.  Special-node forks move the in-register lineage
+// state x as the leaf forks do.
+// ---------------------------------------------------------------------------
+constexpr int BX_PLAIN = 0, BX_R0 = 1, BX_R1 = 2, BX_REP = 3;
+
+// One special node of t = 2 or 4 elements for one frame set: its symbols are
+// nibbles `base`/4.. of x[1], its quanta row q[sym] = lane sym of Vq.
+// Returns the node's partial-sum bits (the codeword the reference writes to
+// ucap: R0 zeros, REP all equal, R1 the hard decisions with the layers' flips).
+template <class Path>
+__device__ __forceinline__ uint32_t bx_spec(Path &st, uint32_t (&x)[2], int type, int t, int base, double Vq, int gl,
+                                            int gbase, int L, int lane, int *sel, int sj) {
+    double l[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) l[j] = shfld(Vq, (int)((x[1] >> (base + 4 * j)) & 15u));  // (j >= t: unused)
+    if (type == BX_R0) {  // :83-98, (float)(l<0)·|l| as a select (H5: element order)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (j < t) st.pm += l[j] < 0 ? fabs(l[j]) : 0.0;
+        return 0u;
+    }
+    if (type == BX_REP) {  // :169-213: the all-zeros / all-ones codewords as keep / flip
+        double kk = st.pm, kf = st.pm;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (j < t) {
+                kk += l[j] < 0 ? fabs(l[j]) : 0.0;
+                kf += l[j] >= 0 ? fabs(l[j]) : 0.0;
+            }
+        if (keep_all8(__builtin_bit_cast(uint64_t, kk), __builtin_bit_cast(uint64_t, kf), gl)) {
+            st.pm = kk;
+            return 0u;
+        }
+        const Sel sx = select_survivors8(kk, kf, gl, gbase, lane, sel, sj);
+        const int p = gbase + sx.parent;
+        st.pm = pick(sx.upper, shfld(kf, p), shfld(kk, p));
+        st.move(p);
+        x[0] = (uint32_t)lane_read((int)x[0], p);
+        x[1] = (uint32_t)lane_read((int)x[1], p);
+        return sx.upper ? (1u << t) - 1u : 0u;
+    }
+    // R1 (:100-166): the stable argsort of |l| (std::sort of <= 16 elements is
+    // an insertion sort, H1), packed with the lineage: r = ord (2 bits per rank)
+    // | the ranked elements' symbols (4 bits each, from bit 8) | the decisions
+    // (from bit 24, hard decisions l < 0, flipped per layer).  r follows the
+    // survivors; a layer's flip position is the slot's own ord (H2).
+    uint32_t r = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (j < t) {
+            const double aj = fabs(l[j]);
+            int rk = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (i < t && i != j) rk += (fabs(l[i]) < aj) || (fabs(l[i]) == aj && i < j);
+            r |= ((uint32_t)j << (2 * rk)) | ((((x[1] >> (base + 4 * j)) & 15u)) << (8 + 4 * rk)) |
+                 ((uint32_t)(l[j] < 0) << (24 + j));
+        }
+    }
+    const int m = (L - 1) < t ? (L - 1) : t;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (q < m) {
+            const double ms = fabs(shfld(Vq, (int)((r >> (8 + 4 * q)) & 15u)));
+            const double kf = st.pm + ms;
+            // identity in every group: the later layers' flips are no smaller (ascending |l|)
+            if (keep_all8(__builtin_bit_cast(uint64_t, st.pm), __builtin_bit_cast(uint64_t, kf), gl)) break;
+            const Sel sx = select_survivors8(st.pm, kf, gl, gbase, lane, sel, sj);
+            const int p = gbase + sx.parent;
+            st.pm = pick(sx.upper, shfld(kf, p), shfld(st.pm, p));
+            st.move(p);
+            x[0] = (uint32_t)lane_read((int)x[0], p);
+            x[1] = (uint32_t)lane_read((int)x[1], p);
+            // H2: the flip position is this slot's own ord[q] before the move
+            // (sorted_absllr_idx[i][layer], :136-140), the decisions the parent's
+            const uint32_t own = (r >> (2 * q)) & 3u;
+            r = (uint32_t)lane_read((int)r, p);
+            if (sx.upper) r ^= 1u << (24 + own);
+        }
+    }
+    return (r >> 24) & ((1u << t) - 1u);
+}
+
+// Operands of one leaf slot k (the pair under q3 + k): the table the half's W2
+// comes from (k even: q0's f for k = 0, g for k = 2), the size-4 node's f (k
+// even) or g table, the pair node's f and g tables, and the quanta register
+// (lanes 0-15: the size-4 special node's row, the size-2 special node's row,
+// or the left leaf's row; lanes 16-31: the right leaf's row).
+struct BxSlot {
+    uint32_t t2, t1, tf, tg;
+    double V;
+};
+
+__device__ __forceinline__ BxSlot bx_load(const FastPlan &P, const MOp &op, int k, int ty, int lane) {
+    const int p0 = op.tab, p1 = 2 * p0 + 1, p3 = 4 * p0 + 3;
+    const int h = k >> 1, sub = k & 1;
+    const int t4 = (ty >> (2 * h)) & 3, t2 = (ty >> (4 + 2 * k)) & 3;
+    BxSlot s;
+    s.t2 = 0u;
+    if (!sub) s.t2 = h ? tab_ld(P.g_tab, p0 * 64, lane) : tab_ld(P.f_tab, p0 * 32, lane & 31);
+    s.t1 = sub ? tab_ld(P.g_tab, (p1 + h) * 64, lane) : tab_ld(P.f_tab, (p1 + h) * 32, lane & 31);
+    s.tf = tab_ld(P.f_tab, (p3 + k) * 32, lane & 31);
+    s.tg = tab_ld(P.g_tab, (p3 + k) * 64, lane);
+    // quanta rows vcl[row][pos][sym]: node8 = op.node (the subtree root at depth n-3)
+    const int n = P.n, N = P.N, v = P.v, sym = lane & 15, j = (lane >> 4) & 1;
+    const int pos8 = 8 * op.node;
+    int row = n - 1, pos = pos8 + 2 * k + j;  // leaf rows
+    if (t4 != BX_PLAIN) row = n - 3, pos = pos8 + 4 * h;  // size-4 special node (row d - 1, H3)
+    else if (t2 != BX_PLAIN) row = n - 2, pos = pos8 + 2 * k;
+    s.V = sym < v ? P.vcl[((size_t)row * N + pos) * v + sym] : 0.0;
+    return s;
+}
+
+template <bool LT, int NS, class Path>
+__device__ __forceinline__ void botx_op(const FastPlan &P, const Mem (&M)[NS], const MOp &op, const int32_t *const (&y)[NS],
+                                        Path (&st)[NS], uint32_t Tf0, uint32_t T2, int gl, int gbase, int L, int *sel,
+                                        int sstride, int lane, uint8_t *tb) {
+    const int fr = op.cnt & 0xff, ty = (op.cnt >> 8) & 0xfff;
+    uint32_t x[NS][2], c[NS], c3r[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) x[s][1] = c3r[s] = 0u;
+    if (op.flags & MF_BFG) {  // the depth n-4 parent's f / g folded in (as bot3_op)
+        const bool sl = op.flags & MF_SRC_LDS, ul = op.flags & MF_U_LDS;
+        if constexpr (LT) stage_tab(tb, T2, (op.flags & MF_BG) ? lane : (lane & 31));
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const int src = gbase + pfield(st[s].ps, op.sh_src);
+            const uint32_t a = M[s].ld(sl, op.src_row, src), b = M[s].ld(sl, op.src_row + 1, src);
+            const uint32_t ub = (op.flags & MF_BG) ? M[s].ld(ul, op.u_row, gbase + pfield(st[s].U(), op.sh_u)) : 0u;
+            x[s][0] = LT ? lut_lds<8, true>(tb, a, b, ub) : lut_vec<8>(T2, a, b, ub);
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) x[s][0] = sym_word(P, M[s], op, y[s], gbase + pfield(st[s].ps, op.sh_src), 0);
+    }
+    (void)Tf0;
+#pragma unroll 1  // (unrolled: 18 % slower)
+    for (int k = 0; k < 4; ++k) {
+        const int h = k >> 1, sub = k & 1;
+        const int t4 = (ty >> (2 * h)) & 3, t2 = (ty >> (4 + 2 * k)) & 3;
+        if (t4 != BX_PLAIN && sub) continue;  // the half's size-4 special node ran at slot k - 1
+        // the slot's operands (loaded one slot ahead: 25 % slower through the registers it holds)
+        const BxSlot cur = bx_load(P, op, k, ty, lane);
+        if (!sub) {
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {  // W2 = f(W3) / g(W3, c3) (q0, SCLLUTDecoder.cpp:83-89 / :157-164)
+                const uint32_t w2 = lut_vec<4>(cur.t2, x[s][0], x[s][0] >> 16, h ? (x[s][1] >> 27) & 15u : 0u);
+                x[s][1] = (x[s][1] & (15u << 27)) | w2;
+            }
+        }
+        if (t4 != BX_PLAIN) {  // q1 / q2 special
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                if (s) lds_order();
+                const uint32_t res = bx_spec(st[s], x[s], t4, 4, 0, cur.V, gl, gbase, L, lane, sel + sstride * s, NS * sstride);
+                if (h) c3r[s] = res;
+                else x[s][1] = (x[s][1] & ~(15u << 27)) | (res << 27);
+            }
+            continue;
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {  // W1 = f(W2) / g(W2, c2) (q1 / q2)
+            const uint32_t w2 = x[s][1] & 0xffffu;
+            const uint32_t w1 = sub ? g_pair(cur.t1, (x[s][1] >> 25) & 3u, w2) : f_pair(cur.t1, 0u, w2);
+            x[s][1] = (x[s][1] & ~(0xffu << 16)) | (w1 << 16);
+        }
+        if (t2 == BX_PLAIN) {
+            bot_pair<true, true, false>(st, x, cur.tf, 0, cur.tg, cur.V, 0, fr >> (2 * k), gl, gbase, L, lane, sel, sstride, c);
+        } else {
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                if (s) lds_order();
+                c[s] = bx_spec(st[s], x[s], t2, 2, 16, cur.V, gl, gbase, L, lane, sel + sstride * s, NS * sstride);
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (!sub) {
+                x[s][1] = (x[s][1] & ~(3u << 25)) | (c[s] << 25);
+            } else {
+                const uint32_t c2 = (x[s][1] >> 25) & 3u;
+                const uint32_t c3 = (c2 ^ c[s]) | (c[s] << 2);  // combine at depth n-2
+                if (h) c3r[s] = c3;
+                else x[s][1] = (x[s][1] & ~(15u << 27)) | (c3 << 27);
+            }
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {  // as the end of bot3_op
+        const uint32_t c3l = (x[s][1] >> 27) & 15u;
+        uint32_t res = (c3l ^ c3r[s]) | (c3r[s] << 4);  // combine at depth n-3
+        if (op.flags & MF_BCOMB)
+            res = ((M[s].ld(op.flags & MF_U_LDS, op.u_row, gbase + pfield(st[s].U(), op.sh_u)) & 0xFFu) ^ res) | (res << 8);
+        if (op.flags & MF_BC2) {
+            const int e = op.pad1;
+            res = ((M[s].ld(op.flags & MF_BC2_ULDS, op.r_row, gbase + pfield(st[s].U(), e & 255)) & 0xFFFFu) ^ res) |
+                  (res << 16);
+            M[s].st(op.flags & MF_BC2_DLDS, e >> 16, lane, res);
+            if (!(op.flags & MF_BC2_TOR)) st[s].U() = pset(st[s].U(), (e >> 8) & 255, gl);
+            continue;
+        }
+        M[s].st(op.flags & MF_DST_LDS, op.dst_row, lane, res);
+        if (!(op.flags & MF_TO_R)) st[s].U() = pset(st[s].U(), op.sh_dst, gl);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Special nodes of the Fast decoders (FastSCLUT.cpp:46-107,
 // FastSCLLUTDecoder.cpp:82-213).  The node's symbols are read a word (8
 // symbols) at a time and their quanta vcl[d-1][pos][sym] (H3) fetched 8 at a
@@ -976,7 +1198,7 @@ __device__ __forceinline__ uint32_t r1_layers(Path &st, int *sel, int sj, int gl
 
 template <bool L8, class Path>
 __device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const MOp &op, Path &st, int *sel, int sj,
-                                         int gl, int gbase, int L, int lane, int temp) {
+                                         int gl, int gbase, int L, int lane, int temp, uint32_t *lds_wave) {
     const int src = gbase + pfield(st.ps, op.sh_src);
     const bool sl = op.flags & MF_SRC_LDS;
     const int v = P.v;
@@ -1038,7 +1260,10 @@ __device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const 
             }
         }
     } else {
-        const LdsSeq16 seq{(uint16_t *)(M.lds + M.rw(op.u_row) + lane), M.ns * 128};
+        // the wave's whole LDS tail from the sets' row u_row on (the rows of depths > d and the
+        // selection scratch of every set: free while this node runs; the sets run one after the
+        // other), one 64-lane row per two entries
+        const LdsSeq16 seq{(uint16_t *)(lds_wave + M.rw(op.u_row) + lane), 128};
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
             if (j < temp) {
@@ -1148,7 +1373,7 @@ __device__ __forceinline__ void r1_large(const FastPlan &P, const Mem &M, const 
 // scratch (+3 % FastSCL-LUT at N = 1024 without it).
 template <bool kList, bool L8, bool R1L, class Path>
 __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, const MOp &op, Path &st, int *sel, int sj,
-                                           int gl, int gbase, int L, int lane) {
+                                           int gl, int gbase, int L, int lane, uint32_t *lds_wave) {
     const int fl = op.flags;
     const int temp = op.cnt;
     const int src = gbase + pfield(st.ps, op.sh_src);
@@ -1268,7 +1493,7 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
             }
         }
     } else if (temp <= stl::kThreshold || (fl & MF_R1_LDS)) {
-        r1_small<L8>(P, M, op, st, sel, sj, gl, gbase, L, lane, temp);
+        r1_small<L8>(P, M, op, st, sel, sj, gl, gbase, L, lane, temp, lds_wave);
     } else if constexpr (R1L) {
         r1_large(P, M, op, st, sel, gl, gbase, L, lane, temp);
     }
@@ -1319,21 +1544,21 @@ __device__ unsigned long long qpd_stamp_acc[64];
 // PW1: one pointer word per path (PathT; the host packed the op list's fields).
 template <int KIND, int NS, bool L8, bool R1L = false, bool PFX = false, bool PW1 = false>
 __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
-                                : NS == 2 ? (KIND == K_SCL_LUT && !PFX ? QPD_WPE2_SCL : QPD_WPE2)
+                                : NS == 2 ? ((KIND == K_SCL_LUT || KIND == K_FASTSCL_LUT) && !PFX ? QPD_WPE2_SCL : QPD_WPE2)
                                 : KIND == K_FASTSCL_LUT ? QPD_WPE_FSCL : QPD_WPE1) void lut_fast_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
                                                                uint8_t *__restrict__ out,
                                                                const MOp *__restrict__ ops) {
     constexpr bool kList = (KIND == K_SCL_LUT || KIND == K_FASTSCL_LUT);
-    // staged BOT3 loads + the speculative right-leaf lookup: SCL-LUT (the
-    // FastSCL-LUT unit measured 15-25 % slower with them, r04h)
-    constexpr bool kLazy = QPD_BOT3_LAZY && KIND == K_SCL_LUT;
+    // staged BOT3 loads: the list kinds (SCL-LUT, FastSCL-LUT)
+    constexpr bool kLazy = QPD_BOT3_LAZY && kList;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
     // rows of all sets interleaved, each set's selection scratch as its next two
     // rows: set s's slots at sel_all + s * 64, its junk slots NS * 64 words on
     const int sstride = 64;
     int *const sel_all = (int *)(lds_dyn + NS * P.lds_rows * 64);
-    // SCL-LUT: the f / g ops' byte tables (stage_tab), 768 B after the selection scratch
-    constexpr bool kLdsTab = KIND == K_SCL_LUT && NS >= 2;
+    // list kinds at two frame sets: the f / g ops' byte tables (stage_tab), 768 B after
+    // the selection scratch, and the folded descents (MF_FF)
+    constexpr bool kLdsTab = kList && NS >= 2;
     uint8_t *const tb = (uint8_t *)(sel_all + NS * kSelInts);
     Mem Mv[NS];
     {
@@ -1423,6 +1648,13 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
             const int fl = op.flags;
             switch (op.type) {
                 case OP_BOT3:
+                    if constexpr (KIND == K_FASTSCL_LUT && L8 && !QPD_EXP_NO_BOTX) {
+                        if (fl & MF_BOTX) {
+                            if (kLazy && oi + 1 < P.nops) pre = fetch_pre(P, nxt, lane, vlane);
+                            botx_op<kLdsTab>(P, Mv, op, yv, stv, cur.T, cur.T2, gl, gbase, L, sel_all, sstride, lane, tb);
+                            break;
+                        }
+                    }
                     bot3_op<kList, L8, kLazy, kLdsTab>(P, Mv, op, yv, stv, cur.T, cur.T2, gl, gbase, L, sel_all, sstride, lane, [&]() {
                         if (oi + 1 < P.nops) pre = fetch_pre(P, nxt, lane, vlane);
                     }, tb);
@@ -1435,7 +1667,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                         src[s] = gbase + pfield(stv[s].ps, op.sh_src);
                         usrc[s] = gbase + pfield(stv[s].U(), op.sh_u);
                     }
-                    if constexpr (KIND == K_SCL_LUT && NS >= 2) {
+                    if constexpr (kLdsTab) {
                         if (fl & MF_FF) {  // + the left child's f (fuse_descent)
                             const int key = ((fl & MF_DST_LDS) ? 1 : 0) | ((fl & MF_FF_DL) ? 2 : 0);
                             stage_tab(tb, cur.T, op.type == OP_F ? (lane & 31) : lane);
@@ -1604,10 +1836,13 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                 default: if constexpr (KIND == K_FASTSC_LUT || KIND == K_FASTSCL_LUT) {  // special nodes, FastSCLUT.cpp:46-107 / FastSCLLUTDecoder.cpp:82-213
 #pragma unroll
                   for (int s = 0; s < NS; ++s) {
+                    // the sets one after the other: no set's loads hoisted into the other's
+                    // code (their special-node state would be live together)
+                    if (s) lds_order();
                     auto &st = stv[s];
                     const Mem &M = Mv[s];
                     int *const sel = sel_all + sstride * s;
-                    special_op<kList, L8, R1L>(P, M, op, st, sel, NS * sstride, gl, gbase, L, lane);
+                    special_op<kList, L8, R1L>(P, M, op, st, sel, NS * sstride, gl, gbase, L, lane, lds_dyn);
                   }
                   break;
                 }

@@ -1,0 +1,16 @@
+// qpd_fast_fscl1.hip -- the FastSCL-LUT decode kernel with one pointer word per
+// path, two frame sets and L = 8 (lut_fast_kernel<K_FASTSCL_LUT, 2, true, false,
+// false, true>, qpd_fast.hip): the config-C4 bench kernel.  See qpd_k_fast.hip.
+#if !defined(QPD_STAMPS) || defined(QPD_UNIT_INCLUDED)
+#define QPD_FAST_TEMPLATES_ONLY
+#include "qpd_fast.hip"
+
+namespace qpd {
+
+const void *fast_kernel_fscl_pw1(int sets, bool l8, bool r1l) {
+    if (sets != 2 || !l8 || r1l) return nullptr;
+    return reinterpret_cast<const void *>(&lut_fast_kernel<K_FASTSCL_LUT, 2, true, false, false, true>);
+}
+
+}  // namespace qpd
+#endif

@@ -1,3 +1,4 @@
+#pragma once
 // qpd_generic.hip -- generic gfx950 engine: every decoder of the reference,
 // LUT symbols or fp64 LLRs, any table layout.
 //

@@ -193,11 +193,14 @@ def minsum_uniform_luts(N: int, v: int = 16, delta: float = 0.5, rows: int | Non
 
 
 def random_luts(N: int, v: int = 16, seed: int = 0, distinct_mags: int | None = 4,
-                per_element: bool = False, rows: int | None = None) -> PackedLUT:
+                per_element: bool = False, rows: int | None = None, node_rows: bool = False) -> PackedLUT:
     """Random tables (every entry uniform in [0, v)) and random vcl drawn from
     ``distinct_mags`` magnitudes with random signs -- a tie-heavy stress input for
     the path-metric sort (hazard H1).  ``distinct_mags=None`` draws continuous
-    values.  ``per_element`` makes every element of every node use its own table."""
+    values.  ``per_element`` makes every element of every node use its own table.
+    ``node_rows``: the elements of each node share one quanta row, as the
+    MinDistortion generator makes them (row r is read by the special nodes of
+    depth r + 1, so its positions are grouped by those nodes)."""
     n = _log2(N)
     rng = np.random.default_rng(seed)
     rows = n + 1 if rows is None else rows
@@ -225,5 +228,9 @@ def random_luts(N: int, v: int = 16, seed: int = 0, distinct_mags: int | None = 
         vcl = np.where(zero, 0.0, mags * rng.choice([-1.0, 1.0], size=(rows, N, v)))
     else:
         vcl = rng.normal(0, 3, size=(rows, N, v))
+    if node_rows:  # one row per node of depth r + 1: copy each group's first row
+        for r in range(rows):
+            g = max(1, N >> (r + 1))
+            vcl[r] = np.repeat(vcl[r, ::g], g, axis=0)[:N]
     return PackedLUT(N=N, v=v, lut_f=lut_f, f_base=f_base, f_step=step, lut_g=lut_g, g_base=g_base,
                      g_step=step, vcl=np.ascontiguousarray(vcl), deduplicated=not per_element)

@@ -10,12 +10,24 @@ OUT="$ROOT/build_variants"
 mkdir -p "$OUT/obj_$NAME"
 SRC="${QPD_VARIANT_SRC:-$ROOT/quantized_decoder_polar_codes_amd/csrc}"  # another tree: QPD_VARIANT_SRC=DIR/csrc
 CXX="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I${QPD_VARIANT_INC:-$ROOT/include} -I$SRC $*"
-$CXX -c "$SRC/qpd_capi.hip" -o "$OUT/obj_$NAME/capi.o" -Rpass-analysis=kernel-resource-usage > "$OUT/obj_$NAME/capi.log" 2>&1 &
-$CXX -mllvm -amdgpu-sched-strategy=${FSCL_SCHED:-max-ilp} -c "$SRC/qpd_fast_fscl.hip" -o "$OUT/obj_$NAME/fscl.o" -Rpass-analysis=kernel-resource-usage > "$OUT/obj_$NAME/fscl.log" 2>&1 &
-$CXX -c "$SRC/qpd_lutgen.cpp" -o "$OUT/obj_$NAME/lutgen.o" > "$OUT/obj_$NAME/lutgen.log" 2>&1 &
+UNITS=$(cd "$ROOT" && python3 -c "
+from quantized_decoder_polar_codes_amd import build
+for u, fl in build.UNITS: print(u + '|' + ' '.join(fl))")
+# VARIANT_UNITS="a.hip b.hip": compile only those, link the rest from the last
+# in-tree build (build/obj, build.py)
+objs=()
+while IFS='|' read -r u fl; do
+  o="$OUT/obj_$NAME/${u%.*}.o"
+  [ -f "$SRC/$u" ] || continue
+  if [ -n "${VARIANT_UNITS:-}" ] && [[ " $VARIANT_UNITS " != *" $u "* ]]; then
+    objs+=("$ROOT/build/obj/${u%.*}.o"); continue
+  fi
+  $CXX $fl -c "$SRC/$u" -o "$o" -Rpass-analysis=kernel-resource-usage > "$OUT/obj_$NAME/${u%.*}.log" 2>&1 &
+  objs+=("$o")
+done <<< "$UNITS"
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$OUT/obj_$NAME/capi.o" "$OUT/obj_$NAME/fscl.o" "$OUT/obj_$NAME/lutgen.o" -o "$OUT/libqpd_$NAME.so"
-cat "$OUT/obj_$NAME/capi.log" "$OUT/obj_$NAME/fscl.log" | grep -A10 "Function Name: _ZN3qpd15lut_fast_kernel" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "${objs[@]}" -o "$OUT/libqpd_$NAME.so"
+cat "$OUT"/obj_$NAME/*.log | grep -A10 "Function Name: _ZN3qpd15lut_fast_kernel" \
   | grep -E "Function Name|VGPRs:|ScratchSize|SGPRs Spill" | sed 's/.*remark: //; s/\[-Rpass.*//' | paste - - - - \
   | sed "s/Function Name: _ZN3qpd15lut_fast_kernel/  /"
 rm -rf "$OUT/obj_$NAME"
