@@ -16,8 +16,7 @@
 #include "qpd_fast.hip"
 
 // Kernel instantiations, each in its own translation unit (build.py UNITS:
-// the units compile in parallel).  Diagnostic builds that read device
-// globals (QPD_STAMPS) compile them into this unit instead (the end of the file).
+// the units compile in parallel).
 namespace qpd {
 const void *fast_kernel_single(int kind, int sets);              // qpd_k_fast.hip
 const void *prefix_kernel(int kind, int sets, bool pw1);         // qpd_k_fast.hip
@@ -1053,8 +1052,22 @@ int init_task_queue(qpd_decoder *d) {
     return QPD_OK;
 }
 
+#ifdef QPD_STAMPS
+// Diagnostic builds: the per-op-class cycle accumulators every decoder's
+// kernels add to (qpd_debug_stamps), one device buffer per process.
+unsigned long long *stamp_buffer() {
+    static unsigned long long *buf = nullptr;
+    if (!buf && hipMalloc(&buf, 64 * sizeof(unsigned long long)) == hipSuccess)
+        (void)hipMemset(buf, 0, 64 * sizeof(unsigned long long));
+    return buf;
+}
+#endif
+
 int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     qpd::FastPlan &F = d->fplan;
+#ifdef QPD_STAMPS
+    F.stamps = stamp_buffer();
+#endif
     const int N = c->N, n = d->n, v = c->v;
     F.N = N;
     F.n = n;
@@ -1270,6 +1283,9 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
         if (rc) return rc;
         d->main_ops_host = mops;  // the import ops get the record buffers' addresses (patch_imports)
     }
+    for (const qpd::MOp &m : mops)  // the kernel's f / g ops have no (S[d] in LDS, S[d+1] in the slab) variant
+        if ((m.type == qpd::OP_F || m.type == qpd::OP_G) && (m.flags & qpd::MF_SRC_LDS) && !(m.flags & qpd::MF_DST_LDS))
+            return fail(QPD_E_INVALID, "fast plan: an f/g op reads LDS rows and writes slab rows");
     F.nops = (int)mops.size();
     d->num_mops = F.nops + d->pfx_nops + d->pfx2_nops;
     {
@@ -2152,20 +2168,12 @@ int qpd_kernel_times(qpd_decoder *d, double *ms, int64_t *launches) {
 // cycle / count accumulators of lut_fast_kernel.
 int qpd_debug_stamps(unsigned long long *out64) {
     QPD_HIP(hipDeviceSynchronize());
-    QPD_HIP(hipMemcpyFromSymbol(out64, HIP_SYMBOL(qpd::qpd_stamp_acc), 64 * sizeof(unsigned long long)));
-    static const unsigned long long zero[64] = {0};
-    QPD_HIP(hipMemcpyToSymbol(HIP_SYMBOL(qpd::qpd_stamp_acc), zero, sizeof(zero)));
+    unsigned long long *acc = stamp_buffer();
+    if (!acc) return fail(QPD_E_DEVICE, "stamp buffer");
+    QPD_HIP(hipMemcpy(out64, acc, 64 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    QPD_HIP(hipMemset(acc, 0, 64 * sizeof(unsigned long long)));
     return QPD_OK;
 }
 #endif
 }  // extern "C"
 
-#ifdef QPD_STAMPS  // (see the declarations at the top)
-#define QPD_UNIT_INCLUDED
-#include "qpd_k_fast.hip"
-#include "qpd_k_scl.hip"
-#include "qpd_k_scl1.hip"
-#include "qpd_fast_fscl.hip"
-#include "qpd_fast_fscl1.hip"
-#include "qpd_k_generic.hip"
-#endif

@@ -119,6 +119,9 @@ struct FastPlan {
     // cost it SGPRs (spill 149 -> 158).
     uint32_t *pfx;
     int32_t pfx_rec, pfx_geo, pm_off;
+#ifdef QPD_STAMPS
+    unsigned long long *stamps;   // diagnostic builds: [64] per-class cycle / count accumulators
+#endif
 };
 
 // Timing experiments only (wrong results): 0 = every op reads node 0's
@@ -154,6 +157,14 @@ struct Mem {
     int so;                     // this set's byte offset in a slab row group (s * 256)
     int ns;                     // frame sets of the wave: the row stride in rows
     __device__ __forceinline__ int rw(int row) const { return row * ns * 64; }  // words to row `row`
+    // the view of set s (runtime) from set 0's
+    __device__ __forceinline__ Mem set(int s) const {
+        Mem m = *this;
+        m.lds = lds + s * 64;
+        m.gp = gp + s * 64;
+        m.so = so + s * 256;
+        return m;
+    }
     // `row` wave-uniform: it rides in the buffer op's SGPR offset
     __device__ __forceinline__ uint32_t ld(bool in_lds, int row, int lane) const {
         if (in_lds) return lds[rw(row) + lane];
@@ -254,10 +265,31 @@ __device__ __forceinline__ uint32_t chan_word8(const int32_t *y, int e0, bool ve
 }
 
 // Word w (8 symbols) of S[d] of the path whose slot is `src`.
+// The first `cnt` channel symbols as one nibble word, a rolled loop: the
+// channel reads of the ops that see the channel only in codes of N <= 8 (the
+// BOT3 / leaf ops at the root) -- small code for a case that is never hot.
+__device__ __forceinline__ uint32_t chan_small(const int32_t *y, int cnt, int v, int32_t *err) {
+    uint32_t w = 0, bad = 0;
+#pragma unroll 1
+    for (int i = 0; i < cnt; ++i) {
+        const uint32_t s = (uint32_t)y[i];
+        bad |= s >= (uint32_t)v;
+        w |= (s >= (uint32_t)v ? 0u : s) << (4 * i);
+    }
+    if (bad) atomicOr(err, 1);
+    return w;
+}
+
+// Word w of S[d]: the pre-pass row (MF_PRE), a slab / LDS row, or with CH the
+// channel (MF_CHAN): the ops that read the channel only in codes of N <= 8
+// (the BOT3 / leaf ops at the root; word 0, chan_small).  The f / g ops at
+// the root read it in fg_chan_op.
+template <bool CH = false>
 __device__ __forceinline__ uint32_t sym_word(const FastPlan &P, const Mem &M, const MOp &op, const int32_t *y, int src,
                                              int w, int cnt = 8) {
     if (op.flags & MF_PRE) return ((const uint32_t *)y)[op.src_row + w];  // N >= 16: whole words
-    if (op.flags & MF_CHAN) return cnt == 8 ? chan_word8(y, 8 * w, P.in_vec, P.v, P.err) : chan_word(y, 8 * w, cnt, P.v, P.err);
+    if constexpr (CH)
+        if (op.flags & MF_CHAN) return chan_small(y, cnt, P.v, P.err);
     return M.ld(op.flags & MF_SRC_LDS, op.src_row + w, src);
 }
 
@@ -356,6 +388,36 @@ __device__ __forceinline__ uint32_t fg_word(const FastPlan &P, const Mem &M, con
                                             int cnt = 8) {
     if constexpr (RAW) return M.ld(SL >= 0 ? SL != 0 : (op.flags & MF_SRC_LDS) != 0, op.src_row + w, src);
     return sym_word(P, M, op, y, src, w, cnt);
+}
+
+// f / g op at the root on the channel symbols (MF_CHAN: codes without the
+// root pre-pass), a rolled loop over its words -- one copy of the channel
+// reads (range check, error flag) instead of one per unrolled word.
+template <bool ISG, int NS>
+__device__ __forceinline__ void fg_chan_op(const FastPlan &P, const Mem (&M)[NS], const MOp &op, const int32_t *const (&y)[NS],
+                                           const int (&usrc)[NS], uint32_t T, int lane) {
+    const int ctemp = op.cnt;
+    const bool dl = op.flags & MF_DST_LDS, ul = op.flags & MF_U_LDS;
+    if (ctemp >= 8) {
+        const int nwo = ctemp >> 3;
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll 1
+            for (int w = 0; w < nwo; ++w) {
+                const uint32_t a = chan_word8(y[s], 8 * w, P.in_vec, P.v, P.err);
+                const uint32_t b = chan_word8(y[s], 8 * (nwo + w), P.in_vec, P.v, P.err);
+                const uint32_t ub = ISG ? M[s].ld(ul, op.u_row + (w >> 2), usrc[s]) >> ((w & 3) << 3) : 0u;
+                M[s].st(dl, op.dst_row + w, lane, lut_vec<8>(T, a, b, ub));
+            }
+    } else {  // ctemp in {2, 4}: the whole root (a then b) in one word
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const uint32_t W = chan_small(y[s], 2 * ctemp, P.v, P.err);
+            const uint32_t ub = ISG ? M[s].ld(ul, op.u_row, usrc[s]) : 0u;
+            const uint32_t out = ctemp == 4 ? lut_vec<4>(T, W, W >> 16, ub) : lut_vec<2>(T, W, W >> 8, ub);
+            M[s].st(dl, op.dst_row, lane, out);
+        }
+    }
 }
 
 // LT: lookups from the byte table staged at tb (lut_lds) instead of T.
@@ -606,6 +668,31 @@ struct PathT<true> {
     __device__ __forceinline__ void move(int p) { ps = shfl64(ps, p); }
 };
 
+// Move every set's state one slot down (set s + 1 into slot s, slot 0 to the
+// end): a loop over the sets that runs set s in slot 0 has its own state back
+// in place after NS steps.
+template <class T, int NS>
+__device__ __forceinline__ void rotate_sets(T (&a)[NS]) {
+    if constexpr (NS > 1) {
+        T t = a[0];
+#pragma unroll
+        for (int i = 0; i + 1 < NS; ++i) a[i] = a[i + 1];
+        a[NS - 1] = t;
+    }
+}
+template <class T, int NS, int W>
+__device__ __forceinline__ void rotate_sets(T (&a)[NS][W]) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        T c[NS];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) c[i] = a[i][w];
+        rotate_sets(c);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) a[i][w] = c[i];
+    }
+}
+
 constexpr int kSelInts = 128;  // per set: 64 slots + 64 junk slots (select_survivors8): two rows after the set's
 
 // max of two non-negative doubles given as bits (one v_max_f64).
@@ -854,7 +941,7 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
         }
     } else {
 #pragma unroll
-        for (int s = 0; s < NS; ++s) x[s][0] = sym_word(P, M[s], op, y[s], gbase + pfield(st[s].ps, op.sh_src), 0);  // W3
+        for (int s = 0; s < NS; ++s) x[s][0] = sym_word<true>(P, M[s], op, y[s], gbase + pfield(st[s].ps, op.sh_src), 0);  // W3
     }
     // ---- q0 left: W2 = f(W3); q1: W1 = f(W2)
 #pragma unroll
@@ -1060,7 +1147,7 @@ __device__ __forceinline__ void botx_op(const FastPlan &P, const Mem (&M)[NS], c
         }
     } else {
 #pragma unroll
-        for (int s = 0; s < NS; ++s) x[s][0] = sym_word(P, M[s], op, y[s], gbase + pfield(st[s].ps, op.sh_src), 0);
+        for (int s = 0; s < NS; ++s) x[s][0] = sym_word<true>(P, M[s], op, y[s], gbase + pfield(st[s].ps, op.sh_src), 0);
     }
     (void)Tf0;
 #pragma unroll 1  // (unrolled: 18 % slower)
@@ -1078,12 +1165,14 @@ __device__ __forceinline__ void botx_op(const FastPlan &P, const Mem (&M)[NS], c
             }
         }
         if (t4 != BX_PLAIN) {  // q1 / q2 special
-#pragma unroll
+#pragma unroll 1  // (set s in slot 0, see rotate_sets)
             for (int s = 0; s < NS; ++s) {
-                if (s) lds_order();
-                const uint32_t res = bx_spec(st[s], x[s], t4, 4, 0, cur.V, gl, gbase, L, lane, sel + sstride * s, NS * sstride);
-                if (h) c3r[s] = res;
-                else x[s][1] = (x[s][1] & ~(15u << 27)) | (res << 27);
+                const uint32_t res = bx_spec(st[0], x[0], t4, 4, 0, cur.V, gl, gbase, L, lane, sel + sstride * s, NS * sstride);
+                if (h) c3r[0] = res;
+                else x[0][1] = (x[0][1] & ~(15u << 27)) | (res << 27);
+                rotate_sets(st);
+                rotate_sets(x);
+                rotate_sets(c3r);
             }
             continue;
         }
@@ -1096,10 +1185,12 @@ __device__ __forceinline__ void botx_op(const FastPlan &P, const Mem (&M)[NS], c
         if (t2 == BX_PLAIN) {
             bot_pair<true, true, false>(st, x, cur.tf, 0, cur.tg, cur.V, 0, fr >> (2 * k), gl, gbase, L, lane, sel, sstride, c);
         } else {
-#pragma unroll
+#pragma unroll 1
             for (int s = 0; s < NS; ++s) {
-                if (s) lds_order();
-                c[s] = bx_spec(st[s], x[s], t2, 2, 16, cur.V, gl, gbase, L, lane, sel + sstride * s, NS * sstride);
+                c[0] = bx_spec(st[0], x[0], t2, 2, 16, cur.V, gl, gbase, L, lane, sel + sstride * s, NS * sstride);
+                rotate_sets(st);
+                rotate_sets(x);
+                rotate_sets(c);
             }
         }
 #pragma unroll
@@ -1167,7 +1258,7 @@ __device__ __forceinline__ uint32_t r1_layers(Path &st, int *sel, int sj, int gl
                                                      double vrow, const double *vq, int v, uint32_t hw, int temp) {
     uint32_t flips = 0;
     int origin = gl;
-#pragma unroll
+#pragma unroll 1  // (one copy of the fork code)
     for (int layer = 0; layer < kMaxM; ++layer) {
         if (layer < m) {
             const int o = gbase + origin;
@@ -1500,11 +1591,9 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
     if (!(fl & MF_TO_R)) st.U() = pset(st.U(), op.sh_dst, gl);
 }
 
-#ifdef QPD_STAMPS
-// Diagnostic build only: wave cycles per op class (lane k of each wave
-// accumulates class k; flushed once per wave).  Class = 2*type + (op syncs).
-__device__ unsigned long long qpd_stamp_acc[64];
-#endif
+// QPD_STAMPS (diagnostic builds only): wave cycles per op class (lane k of
+// each wave accumulates class k; flushed into FastPlan::stamps once per task).
+// Class = 2*type + (op syncs), or by depth with QPD_STAMPS_DEPTH.
 
 // Waves per SIMD the register allocation targets: 6 (80 VGPRs) for one
 // frame set, 4 (128 VGPRs) for two (5 for SCL-LUT, below), 6 for FastSCL's one set too (its special
@@ -1696,18 +1785,20 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                         if constexpr (kLdsTab)
                             if (op.cnt >= 8) stage_tab(tb, cur.T, op.type == OP_F ? (lane & 31) : lane);
 #define QPD_FG(G, S_, D_) fg_op<G, true, NS, S_, D_, kLdsTab>(P, Mv, op, yv, src, usrc, cur.T, lane, tb)
+                        // (S[d] in LDS puts S[d + 1] in LDS too: no key 1 variant)
                         if (op.type == OP_F) {
                             if (key == 0) QPD_FG(false, 0, 0);
-                            else if (key == 1) QPD_FG(false, 1, 0);
                             else if (key == 2) QPD_FG(false, 0, 1);
                             else QPD_FG(false, 1, 1);
                         } else {
                             if (key == 0) QPD_FG(true, 0, 0);
-                            else if (key == 1) QPD_FG(true, 1, 0);
                             else if (key == 2) QPD_FG(true, 0, 1);
                             else QPD_FG(true, 1, 1);
                         }
 #undef QPD_FG
+                    } else if (fl & MF_CHAN) {
+                        if (op.type == OP_F) fg_chan_op<false>(P, Mv, op, yv, usrc, cur.T, lane);
+                        else fg_chan_op<true>(P, Mv, op, yv, usrc, cur.T, lane);
                     } else if (op.type == OP_F)
                         fg_op<false, false>(P, Mv, op, yv, src, usrc, cur.T, lane);
                     else
@@ -1728,7 +1819,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                         dm[s] = 0;
                         none[s][0] = 0;
                         if (kList || !frozen) {
-                            const uint32_t W = sym_word(P, Mv[s], op, yv[s], gbase + pfield(stv[s].ps, op.sh_src), 0, 2);
+                            const uint32_t W = sym_word<true>(P, Mv[s], op, yv[s], gbase + pfield(stv[s].ps, op.sh_src), 0, 2);
                             uint32_t idx = ((W & 15u) << 4) | ((W >> 4) & 15u);
                             if (right)
                                 idx |= (Mv[s].ld(fl & MF_U_LDS, op.u_row, gbase + pfield(stv[s].U(), op.sh_u)) & 1u) << 8;
@@ -1834,15 +1925,14 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                     }
                     break;
                 default: if constexpr (KIND == K_FASTSC_LUT || KIND == K_FASTSCL_LUT) {  // special nodes, FastSCLUT.cpp:46-107 / FastSCLLUTDecoder.cpp:82-213
-#pragma unroll
+                  // the sets one after the other, one copy of the code: set s runs in
+                  // stv[0] (the sets' states rotate; back in place after NS steps) --
+                  // the special nodes' code is not in the instruction cache twice
+#pragma unroll 1
                   for (int s = 0; s < NS; ++s) {
-                    // the sets one after the other: no set's loads hoisted into the other's
-                    // code (their special-node state would be live together)
-                    if (s) lds_order();
-                    auto &st = stv[s];
-                    const Mem &M = Mv[s];
-                    int *const sel = sel_all + sstride * s;
-                    special_op<kList, L8, R1L>(P, M, op, st, sel, NS * sstride, gl, gbase, L, lane, lds_dyn);
+                    special_op<kList, L8, R1L>(P, Mv[0].set(s), op, stv[0], sel_all + sstride * s, NS * sstride, gl, gbase,
+                                               L, lane, lds_dyn);
+                    rotate_sets(stv);
                   }
                   break;
                 }
@@ -1854,7 +1944,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
 #ifdef QPD_STAMPS_DEPTH  // F / G / COMB by depth: 0-7 / 8-15 / 16-23; BOT3 24; leaves 25; specials 26-29
                 const int dd = op.d < 7 ? op.d : 7;
                 const int cls = op.type == OP_F ? dd : op.type == OP_G ? 8 + dd : op.type == OP_COMB ? 16 + dd
-                              : op.type == OP_BOT3 ? 24 : (op.type == OP_LEAF_L || op.type == OP_LEAF_R) ? 25
+                              : op.type == OP_BOT3 ? ((fl & MF_BOTX) ? 30 : 24) : (op.type == OP_LEAF_L || op.type == OP_LEAF_R) ? 25
                               : 26 + (op.type - OP_R0) % 4;
 #else
                 const int cls = op.type == OP_R1 ? 24 + (op.cnt > 16) + (op.cnt > 8) : 2 * op.type + ((fl & MF_SYNC) ? 1 : 0);
@@ -1994,8 +2084,8 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
         if (threadIdx.x == 31) stamp_acc += __builtin_amdgcn_s_memtime() - stamp_t2;  // class 31: frame tail
         if (threadIdx.x == 31) stamp_cnt += 1;
         if (threadIdx.x < 32) {
-            atomicAdd(&qpd_stamp_acc[threadIdx.x], (unsigned long long)stamp_acc);
-            atomicAdd(&qpd_stamp_acc[32 + threadIdx.x], (unsigned long long)stamp_cnt);
+            atomicAdd(&P.stamps[threadIdx.x], (unsigned long long)stamp_acc);
+            atomicAdd(&P.stamps[32 + threadIdx.x], (unsigned long long)stamp_cnt);
         }
 #endif
     }

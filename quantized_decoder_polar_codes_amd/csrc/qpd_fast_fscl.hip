@@ -4,7 +4,6 @@
 // folded descents and combines -- with the special-node ops of
 // FastSCLLUTDecoder.cpp:82-213 and the mixed bottom subtrees (botx_op)
 // compiled in (KIND = K_FASTSCL_LUT).  See qpd_k_fast.hip for the units.
-#if !defined(QPD_STAMPS) || defined(QPD_UNIT_INCLUDED)
 #define QPD_FAST_TEMPLATES_ONLY
 #include "qpd_fast.hip"
 
@@ -22,4 +21,3 @@ const void *fast_kernel_fscl(int sets, bool l8, bool r1l) {
 }
 
 }  // namespace qpd
-#endif

@@ -1,7 +1,6 @@
 // qpd_fast_fscl1.hip -- the FastSCL-LUT decode kernel with one pointer word per
 // path, two frame sets and L = 8 (lut_fast_kernel<K_FASTSCL_LUT, 2, true, false,
 // false, true>, qpd_fast.hip): the config-C4 bench kernel.  See qpd_k_fast.hip.
-#if !defined(QPD_STAMPS) || defined(QPD_UNIT_INCLUDED)
 #define QPD_FAST_TEMPLATES_ONLY
 #include "qpd_fast.hip"
 
@@ -13,4 +12,3 @@ const void *fast_kernel_fscl_pw1(int sets, bool l8, bool r1l) {
 }
 
 }  // namespace qpd
-#endif

@@ -4,7 +4,6 @@
 // qpd_k_scl.hip, qpd_k_scl1.hip, qpd_fast_fscl.hip, qpd_fast_fscl1.hip; build.py
 // UNITS) that compile in parallel.  nullptr for a combination that has no
 // instantiation, so the launch fails loudly.
-#if !defined(QPD_STAMPS) || defined(QPD_UNIT_INCLUDED)
 #define QPD_FAST_TEMPLATES_ONLY
 #include "qpd_fast.hip"
 #include "qpd.h"
@@ -31,4 +30,3 @@ const void *prefix_kernel(int kind, int sets, bool pw1) {
 }
 
 }  // namespace qpd
-#endif

@@ -1,7 +1,6 @@
 // qpd_k_generic.hip -- the generic engine's kernel instantiations
 // (generic_decode_kernel, qpd_generic.hip) as a translation unit of their own
 // (build.py UNITS).
-#if !defined(QPD_STAMPS) || defined(QPD_UNIT_INCLUDED)
 #include "qpd_generic.hip"
 #include "qpd.h"
 
@@ -46,4 +45,3 @@ const void *generic_kernel(int fam, int dom, bool wide) {
 }
 
 }  // namespace qpd
-#endif

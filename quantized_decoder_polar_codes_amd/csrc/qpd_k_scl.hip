@@ -1,6 +1,5 @@
 // qpd_k_scl.hip -- SCL-LUT decode kernel instantiations with two pointer words
 // per path (lut_fast_kernel<K_SCL_LUT, NS, L8>, qpd_fast.hip; see qpd_k_fast.hip).
-#if !defined(QPD_STAMPS) || defined(QPD_UNIT_INCLUDED)
 #define QPD_FAST_TEMPLATES_ONLY
 #include "qpd_fast.hip"
 #include "qpd.h"
@@ -18,4 +17,3 @@ const void *fast_kernel_scl(int sets, bool l8) {
 }
 
 }  // namespace qpd
-#endif

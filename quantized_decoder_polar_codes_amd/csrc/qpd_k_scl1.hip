@@ -1,7 +1,6 @@
 // qpd_k_scl1.hip -- SCL-LUT decode kernel instantiations with one pointer word
 // per path (lut_fast_kernel<K_SCL_LUT, NS, L8, false, false, PW1 = true>,
 // qpd_fast.hip; see qpd_k_fast.hip).  The bench workload's kernel.
-#if !defined(QPD_STAMPS) || defined(QPD_UNIT_INCLUDED)
 #define QPD_FAST_TEMPLATES_ONLY
 #include "qpd_fast.hip"
 #include "qpd.h"
@@ -17,4 +16,3 @@ const void *fast_kernel_scl_pw1(int sets, bool l8) {
 }
 
 }  // namespace qpd
-#endif

@@ -43,7 +43,7 @@ for c in range(32):
         continue
     if os.environ.get("STAMPS_DEPTH"):
         nm = "TAIL" if c == 31 else (["F", "G", "COMB"][c // 8] + f" d{c % 8}" if c < 24 else
-                                     {24: "BOT3", 25: "LEAF", 26: "R0", 27: "R1", 28: "REP", 29: "SPC"}[c])
+                                     {24: "BOT3", 25: "LEAF", 26: "R0", 27: "R1", 28: "REP", 29: "SPC", 30: "BOTX"}[c])
     else:
         nm = "TAIL" if c == 31 else ({24: "R1<=8", 25: "R1 9-16", 26: "R1>16"}[c] if 24 <= c <= 26 else
                                   names[c // 2] + ("/sync" if c % 2 else ""))
