@@ -336,6 +336,14 @@ def roofline(args, dec, kt, frames, calls):
                    "pre_kernel_ms": pre_ms / max(1, n_pre), "algorithmic_bytes_per_call": hbm_bytes,
                    "traffic": (kc.get("traffic") or 0) + ((rec or {}).get("kernels", {}).get("root_pre_kernel", {})
                                                           .get("traffic") or 0) or None}}
+    # the rocprof-measured HBM rate of the decode kernel: its PMC traffic per launch (counters.json)
+    # over its launch duration timed here (HIP events)
+    if kc.get("traffic"):
+        kt_s = dec_ms / max(1, n_dec) * 1e-3
+        out["hbm"]["achieved_counters"] = kc["traffic"] / kt_s / 1e9
+        out["hbm"]["frac_counters"] = out["hbm"]["achieved_counters"] / HBM_PEAK_GBS
+        out["hbm"]["counters_note"] = (f"{kname} HBM-side bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, rocprofv3 PMC "
+                                       "passes) / its average launch duration from the HIP events")
     return out
 
 

@@ -136,6 +136,10 @@ struct FastPlan {
 #ifndef QPD_EXP_NO_BOTX
 #define QPD_EXP_NO_BOTX 0  // register-allocation experiments: botx_op compiled out (MF_BOTX ops then wrong)
 #endif
+#ifndef QPD_EXP_FSCL
+#define QPD_EXP_FSCL 0  // code-quality experiments (wrong results for those ops): 2 no special ops,
+                        // 4 no R1, 8 no R1 LDS introsort, 16 no REP
+#endif
 
 #ifndef QPD_SLAB_AUX
 #define QPD_SLAB_AUX 0  // cache-policy bits of the slab's buffer ops (2 = nt)
@@ -1097,6 +1101,97 @@ __device__ __forceinline__ uint32_t bx_spec(Path &st, uint32_t (&x)[2], int type
     return (r >> 24) & ((1u << t) - 1u);
 }
 
+// bx_spec for all the wave's frame sets at once: the sums interleaved element
+// by element, the R1 layers of the sets interleaved (each set stops at its
+// first identity layer) -- the sets' dependency chains overlap.
+template <int NS, class Path>
+__device__ __forceinline__ void bx_spec_multi(Path (&st)[NS], uint32_t (&x)[NS][2], int type, int t, int base, double Vq, int gl,
+                                              int gbase, int lane, int *sel_all, int sstride, uint32_t (&res)[NS]) {
+    auto fork = [&](int s, double keep, double flip, Sel &sx) {  // survivor exchange of set s (keep / flip keys)
+        sx = select_survivors8(keep, flip, gl, gbase, lane, sel_all + sstride * s, NS * sstride);
+        const int p = gbase + sx.parent;
+        st[s].pm = pick(sx.upper, shfld(flip, p), shfld(keep, p));
+        st[s].move(p);
+        x[s][0] = (uint32_t)lane_read((int)x[s][0], p);
+        x[s][1] = (uint32_t)lane_read((int)x[s][1], p);
+        return p;
+    };
+    if (type != BX_R1) {  // R0 (:83-98) / REP (:169-213)
+        double kk[NS], kf[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) kk[s] = kf[s] = st[s].pm;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (j < t)
+#pragma unroll
+                for (int s = 0; s < NS; ++s) {
+                    const double l = shfld(Vq, (int)((x[s][1] >> (base + 4 * j)) & 15u));
+                    kk[s] += l < 0 ? fabs(l) : 0.0;  // H5: element order
+                    if (type == BX_REP) kf[s] += l >= 0 ? fabs(l) : 0.0;
+                }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            res[s] = 0u;
+            if (type == BX_R0 || keep_all8(__builtin_bit_cast(uint64_t, kk[s]), __builtin_bit_cast(uint64_t, kf[s]), gl)) {
+                st[s].pm = kk[s];
+            } else {
+                Sel sx;
+                fork(s, kk[s], kf[s], sx);
+                res[s] = sx.upper ? (1u << t) - 1u : 0u;
+            }
+        }
+        return;
+    }
+    // R1 (:100-166): per set r = ord | ranked symbols | decisions, as bx_spec
+    uint32_t r[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        double a[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = shfld(Vq, (int)((x[s][1] >> (base + 4 * j)) & 15u));
+        r[s] = 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (j < t) {
+                const double aj = fabs(a[j]);
+                int rk = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (i < t && i != j) rk += (fabs(a[i]) < aj) || (fabs(a[i]) == aj && i < j);
+                r[s] |= ((uint32_t)j << (2 * rk)) | (((x[s][1] >> (base + 4 * j)) & 15u) << (8 + 4 * rk)) |
+                        ((uint32_t)(a[j] < 0) << (24 + j));
+            }
+        }
+    }
+    bool done[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) done[s] = false;
+#pragma unroll 1
+    for (int q = 0; q < t; ++q) {  // m = min(L - 1, t) = t (L = 8, t <= 4)
+        double kf[NS];
+        bool all = true;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (done[s]) continue;
+            kf[s] = st[s].pm + fabs(shfld(Vq, (int)((r[s] >> (8 + 4 * q)) & 15u)));
+            done[s] = keep_all8(__builtin_bit_cast(uint64_t, st[s].pm), __builtin_bit_cast(uint64_t, kf[s]), gl);
+            all = all && done[s];
+        }
+        if (all) break;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (done[s]) continue;
+            Sel sx;
+            const int p = fork(s, st[s].pm, kf[s], sx);
+            const uint32_t own = (r[s] >> (2 * q)) & 3u;  // H2: this slot's own ord[q]
+            r[s] = (uint32_t)lane_read((int)r[s], p);
+            if (sx.upper) r[s] ^= 1u << (24 + own);
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) res[s] = (r[s] >> 24) & ((1u << t) - 1u);
+}
+
 // Operands of one leaf slot k (the pair under q3 + k): the table the half's W2
 // comes from (k even: q0's f for k = 0, g for k = 2), the size-4 node's f (k
 // even) or g table, the pair node's f and g tables, and the quanta register
@@ -1135,6 +1230,9 @@ __device__ __forceinline__ void botx_op(const FastPlan &P, const Mem (&M)[NS], c
     uint32_t x[NS][2], c[NS], c3r[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) x[s][1] = c3r[s] = 0u;
+#if QPD_BX_PIPE
+    BxSlot nx = bx_load(P, op, 0, ty, lane);
+#endif
     if (op.flags & MF_BFG) {  // the depth n-4 parent's f / g folded in (as bot3_op)
         const bool sl = op.flags & MF_SRC_LDS, ul = op.flags & MF_U_LDS;
         if constexpr (LT) stage_tab(tb, T2, (op.flags & MF_BG) ? lane : (lane & 31));
@@ -1155,8 +1253,13 @@ __device__ __forceinline__ void botx_op(const FastPlan &P, const Mem (&M)[NS], c
         const int h = k >> 1, sub = k & 1;
         const int t4 = (ty >> (2 * h)) & 3, t2 = (ty >> (4 + 2 * k)) & 3;
         if (t4 != BX_PLAIN && sub) continue;  // the half's size-4 special node ran at slot k - 1
-        // the slot's operands (loaded one slot ahead: 25 % slower through the registers it holds)
+#if QPD_BX_PIPE
+        const BxSlot cur = nx;
+        const int kn = t4 != BX_PLAIN ? k + 2 : k + 1;  // the next slot run
+        if (kn < 4) nx = bx_load(P, op, kn, ty, lane);
+#else
         const BxSlot cur = bx_load(P, op, k, ty, lane);
+#endif
         if (!sub) {
 #pragma unroll
             for (int s = 0; s < NS; ++s) {  // W2 = f(W3) / g(W3, c3) (q0, SCLLUTDecoder.cpp:83-89 / :157-164)
@@ -1165,14 +1268,12 @@ __device__ __forceinline__ void botx_op(const FastPlan &P, const Mem (&M)[NS], c
             }
         }
         if (t4 != BX_PLAIN) {  // q1 / q2 special
-#pragma unroll 1  // (set s in slot 0, see rotate_sets)
+            uint32_t res[NS];
+            bx_spec_multi(st, x, t4, 4, 0, cur.V, gl, gbase, lane, sel, sstride, res);
+#pragma unroll
             for (int s = 0; s < NS; ++s) {
-                const uint32_t res = bx_spec(st[0], x[0], t4, 4, 0, cur.V, gl, gbase, L, lane, sel + sstride * s, NS * sstride);
-                if (h) c3r[0] = res;
-                else x[0][1] = (x[0][1] & ~(15u << 27)) | (res << 27);
-                rotate_sets(st);
-                rotate_sets(x);
-                rotate_sets(c3r);
+                if (h) c3r[s] = res[s];
+                else x[s][1] = (x[s][1] & ~(15u << 27)) | (res[s] << 27);
             }
             continue;
         }
@@ -1185,13 +1286,7 @@ __device__ __forceinline__ void botx_op(const FastPlan &P, const Mem (&M)[NS], c
         if (t2 == BX_PLAIN) {
             bot_pair<true, true, false>(st, x, cur.tf, 0, cur.tg, cur.V, 0, fr >> (2 * k), gl, gbase, L, lane, sel, sstride, c);
         } else {
-#pragma unroll 1
-            for (int s = 0; s < NS; ++s) {
-                c[0] = bx_spec(st[0], x[0], t2, 2, 16, cur.V, gl, gbase, L, lane, sel + sstride * s, NS * sstride);
-                rotate_sets(st);
-                rotate_sets(x);
-                rotate_sets(c);
-            }
+            bx_spec_multi(st, x, t2, 2, 16, cur.V, gl, gbase, lane, sel, sstride, c);
         }
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
@@ -1258,7 +1353,11 @@ __device__ __forceinline__ uint32_t r1_layers(Path &st, int *sel, int sj, int gl
                                                      double vrow, const double *vq, int v, uint32_t hw, int temp) {
     uint32_t flips = 0;
     int origin = gl;
+#if QPD_R1_UNROLL
+#pragma unroll
+#else
 #pragma unroll 1  // (one copy of the fork code)
+#endif
     for (int layer = 0; layer < kMaxM; ++layer) {
         if (layer < m) {
             const int o = gbase + origin;
@@ -1287,9 +1386,15 @@ __device__ __forceinline__ uint32_t r1_layers(Path &st, int *sel, int sj, int gl
     return temp < 32 ? word & ((1u << temp) - 1u) : word;
 }
 
-template <bool L8, class Path>
-__device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const MOp &op, Path &st, int *sel, int sj,
-                                         int gl, int gbase, int L, int lane, int temp, uint32_t *lds_wave) {
+// The argsort half of an R1 node of <= 32 elements (:100-116) for one set:
+// the m smallest |l| in std::sort's order, packed for r1_layers.
+struct R1Prep {
+    uint32_t ordp0, ordp1, symp, hw;
+};
+
+template <class Path>
+__device__ __forceinline__ R1Prep r1_prep(const FastPlan &P, const Mem &M, const MOp &op, const Path &st, int gbase, int L,
+                                          int lane, int temp, uint32_t *lds_wave) {
     const int src = gbase + pfield(st.ps, op.sh_src);
     const bool sl = op.flags & MF_SRC_LDS;
     const int v = P.v;
@@ -1310,7 +1415,7 @@ __device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const 
     int ord[kMaxM];
 #pragma unroll
     for (int q = 0; q < kMaxM; ++q) ord[q] = 0;
-    if (temp <= stl::kThreshold) {
+    if ((QPD_EXP_FSCL & 8) || temp <= stl::kThreshold) {
         // entries rank << 5 | j (< 2^14) two per register; the m smallest by
         // packed 16-bit min trees (v_pk_min_u16), the taken one set to 0xFFFF
         typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -1368,22 +1473,155 @@ __device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const 
         for (int q = 0; q < kMaxM; ++q)
             if (q < m) ord[q] = seq.get(q) & 31;
     }
-    uint32_t ordp0 = 0, ordp1 = 0, symp = 0;
+    R1Prep r{0u, 0u, 0u, hw};
 #pragma unroll
     for (int q = 0; q < kMaxM; ++q) {
         if (q < m) {
             const int k = ord[q] >> 3;
             const uint32_t w = k == 0 ? W[0] : k == 1 ? W[1] : k == 2 ? W[2] : W[3];
-            symp |= ((w >> (4 * (ord[q] & 7))) & 15u) << (4 * q);
+            r.symp |= ((w >> (4 * (ord[q] & 7))) & 15u) << (4 * q);
             if (q < 6)
-                ordp0 |= (uint32_t)ord[q] << (5 * q);
+                r.ordp0 |= (uint32_t)ord[q] << (5 * q);
             else
-                ordp1 = (uint32_t)ord[q];
+                r.ordp1 = (uint32_t)ord[q];
         }
     }
+    return r;
+}
+
+template <bool L8, class Path>
+__device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const MOp &op, Path &st, int *sel, int sj,
+                                         int gl, int gbase, int L, int lane, int temp, uint32_t *lds_wave) {
+    const int v = P.v;
+    const int m = (L - 1) < temp ? (L - 1) : temp;
+    const double *vq = P.vcl + (size_t)op.vrow * v;
+    const bool uni = op.flags & MF_VUNI;
+    const double vrow = uni && (lane & 15) < v ? vq[lane & 15] : 0.0;
+    const R1Prep r = r1_prep(P, M, op, st, gbase, L, lane, temp, lds_wave);
     const uint32_t word =
-        r1_layers<L8>(st, sel, sj, gl, gbase, lane, L, m, ordp0, ordp1, symp, uni, vrow, vq, v, hw, temp);
+        r1_layers<L8>(st, sel, sj, gl, gbase, lane, L, m, r.ordp0, r.ordp1, r.symp, uni, vrow, vq, v, r.hw, temp);
     M.st(op.flags & MF_DST_LDS, op.dst_row, lane, word);
+}
+
+// R1 nodes of <= 32 elements with L = 8 for all the wave's frame sets: the
+// argsorts set by set, then the layers of the sets interleaved (their fork
+// chains overlap), each set stopping at its first identity layer (r1_layers).
+template <int NS, class Path>
+__device__ __forceinline__ void r1_multi(const FastPlan &P, const Mem (&Mv)[NS], const MOp &op, Path (&st)[NS], int *sel_all,
+                                         int sstride, int gl, int gbase, int lane, uint32_t *lds_wave) {
+    const int temp = op.cnt, v = P.v;
+    const int m = kMaxM < temp ? kMaxM : temp;  // L = 8
+    const double *vq = P.vcl + (size_t)op.vrow * v;
+    const bool uni = op.flags & MF_VUNI;
+    const double vrow = uni && (lane & 15) < v ? vq[lane & 15] : 0.0;
+    R1Prep pr[NS];
+#pragma unroll 1
+    for (int s = 0; s < NS; ++s) {  // set s in slot 0 (rotate_sets)
+        pr[0] = r1_prep(P, Mv[0].set(s), op, st[0], gbase, 8, lane, temp, lds_wave);
+        rotate_sets(st);
+        rotate_sets(pr);
+    }
+    uint32_t flips[NS];
+    int origin[NS];
+    bool done[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        flips[s] = 0;
+        origin[s] = gl;
+        done[s] = false;
+    }
+#pragma unroll 1
+    for (int layer = 0; layer < m; ++layer) {
+        double kf[NS];
+        int own[NS];
+        bool all = true;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (done[s]) continue;
+            const int o = gbase + origin[s];
+            own[s] = (int)(layer < 6 ? __builtin_amdgcn_ubfe(pr[s].ordp0, 5 * layer, 5) : pr[s].ordp1);
+            const uint32_t sym = __builtin_amdgcn_ubfe(pr[s].symp, 4 * layer, 4);
+            const double own_ms = fabs(uni ? shfld(vrow, (int)sym) : vq[(size_t)own[s] * v + sym]);
+            kf[s] = st[s].pm + shfld(own_ms, o);
+            done[s] = keep_all8(__builtin_bit_cast(uint64_t, st[s].pm), __builtin_bit_cast(uint64_t, kf[s]), gl);
+            all = all && done[s];
+        }
+        if (all) break;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (done[s]) continue;
+            const int o = gbase + origin[s];
+            const int pos_old = lane_read(own[s], o);  // H2
+            const Sel sl = select_survivors8(st[s].pm, kf[s], gl, gbase, lane, sel_all + sstride * s, NS * sstride);
+            const int p = gbase + sl.parent;
+            st[s].pm = pick(sl.upper, shfld(kf[s], p), shfld(st[s].pm, p));
+            st[s].move(p);
+            origin[s] = lane_read(origin[s], p);
+            flips[s] = (uint32_t)lane_read((int)flips[s], p) ^ (sl.upper ? 1u << (pos_old & 31) : 0u);
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        uint32_t word = (uint32_t)lane_read((int)pr[s].hw, gbase + origin[s]) ^ flips[s];
+        if (temp < 32) word &= (1u << temp) - 1u;
+        Mv[s].st(op.flags & MF_DST_LDS, op.dst_row, lane, word);
+        if (!(op.flags & MF_TO_R)) st[s].U() = pset(st[s].U(), op.sh_dst, gl);
+    }
+}
+
+// R0 / REP nodes with L = 8 for all the wave's frame sets, interleaved element
+// by element (their sums are dependent fp64 chains in the reference's order,
+// H5; the sets' chains overlap).
+template <int NS, class Path>
+__device__ __forceinline__ void r0rep_multi(const FastPlan &P, const Mem (&Mv)[NS], const MOp &op, Path (&st)[NS], int *sel_all,
+                                            int sstride, int gl, int gbase, int lane) {
+    const int fl = op.flags, temp = op.cnt, v = P.v;
+    const bool rep = op.type == OP_REP, sl = fl & MF_SRC_LDS, dl = fl & MF_DST_LDS;
+    const double *vq = P.vcl + (size_t)op.vrow * v;  // row d-1, position temp*node
+    const bool uni = fl & MF_VUNI;
+    const double vr = uni && (lane & 15) < v ? vq[lane & 15] : 0.0;
+    int src[NS];
+    double kk[NS], kf[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        src[s] = gbase + pfield(st[s].ps, op.sh_src);
+        kk[s] = kf[s] = st[s].pm;
+    }
+    const int n8 = (temp + 7) >> 3;
+#pragma unroll 1
+    for (int w = 0; w < n8; ++w) {
+        uint32_t word[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) word[s] = Mv[s].ld(sl, op.src_row + w, src[s]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if (8 * w + i >= temp) break;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const uint32_t sym = (word[s] >> (4 * i)) & 15u;
+                const double l = uni ? shfld(vr, (int)sym) : vq[(size_t)(8 * w + i) * v + sym];
+                kk[s] += l < 0 ? fabs(l) : 0.0;  // :88-95 / :176-180, (l<0)·|l|, (l>=0)·|l| as selects
+                if (rep) kf[s] += l >= 0 ? fabs(l) : 0.0;
+            }
+        }
+    }
+    const int nwo = (temp + 31) >> 5;
+    const uint32_t m = temp < 32 ? ((1u << temp) - 1u) : 0xffffffffu;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        uint32_t fill = 0;
+        if (!rep || keep_all8(__builtin_bit_cast(uint64_t, kk[s]), __builtin_bit_cast(uint64_t, kf[s]), gl)) {
+            st[s].pm = kk[s];  // R0; REP: the identity selection, every path keeps its all-zeros codeword
+        } else {
+            const Sel sx = select_survivors8(kk[s], kf[s], gl, gbase, lane, sel_all + sstride * s, NS * sstride);
+            const int p = gbase + sx.parent;
+            st[s].pm = pick(sx.upper, shfld(kf[s], p), shfld(kk[s], p));
+            st[s].move(p);
+            fill = sx.upper ? 0xffffffffu : 0u;
+        }
+        for (int w = 0; w < nwo; ++w) Mv[s].st(dl, op.dst_row + w, lane, fill & m);
+        if (!(fl & MF_TO_R)) st[s].U() = pset(st[s].U(), op.sh_dst, gl);
+    }
 }
 
 // R1 nodes above 32 elements (N >= 2048 codes) or without LDS room: the
@@ -1488,6 +1726,7 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
         }
     };
     const int n8 = (temp + 7) >> 3;
+    if (QPD_EXP_FSCL & 2) return;
     if (op.type == OP_R0) {
         if (kList) {
             for (int w = 0; w < n8; ++w) {
@@ -1500,7 +1739,7 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
             }
         }
         for (int w = 0; w < nwo; ++w) M.st(dl, op.dst_row + w, lane, 0u);
-    } else if (op.type == OP_REP) {
+    } else if (op.type == OP_REP && !(QPD_EXP_FSCL & 16)) {
         uint32_t fill = 0;
         if (!kList) {
             double S = 0;
@@ -1583,6 +1822,7 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
                 word = 0;
             }
         }
+    } else if (QPD_EXP_FSCL & 4) {
     } else if (temp <= stl::kThreshold || (fl & MF_R1_LDS)) {
         r1_small<L8>(P, M, op, st, sel, sj, gl, gbase, L, lane, temp, lds_wave);
     } else if constexpr (R1L) {
@@ -1614,6 +1854,22 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
 #ifndef QPD_WPE2_SCL
 #define QPD_WPE2_SCL 5
 #endif
+// FastSCL-LUT's two-set kernel: 4 waves per SIMD (128 VGPRs): its special-node
+// and mixed-subtree code cost the whole kernel's allocation at 96 (the SCL-LUT op
+// list on the FastSCL-LUT instantiation: 32.7 M frames/s at 5 waves, 37.7 M at 4,
+// against 45.2 M on the SCL-LUT one; FastSCL-LUT 31.7 -> 37.7 M)
+#ifndef QPD_WPE2_FSCL
+#define QPD_WPE2_FSCL 4
+#endif
+#ifndef QPD_BX_PIPE
+#define QPD_BX_PIPE 0  // BOTX slot operands loaded one slot ahead
+#endif
+#ifndef QPD_SPEC_ROT
+#define QPD_SPEC_ROT 1  // special ops: one code copy, the sets rotated through slot 0 (else unrolled)
+#endif
+#ifndef QPD_R1_UNROLL
+#define QPD_R1_UNROLL 0  // R1 layers unrolled
+#endif
 #ifndef QPD_WPE3
 #define QPD_WPE3 3
 #endif
@@ -1633,7 +1889,7 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
 // PW1: one pointer word per path (PathT; the host packed the op list's fields).
 template <int KIND, int NS, bool L8, bool R1L = false, bool PFX = false, bool PW1 = false>
 __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
-                                : NS == 2 ? ((KIND == K_SCL_LUT || KIND == K_FASTSCL_LUT) && !PFX ? QPD_WPE2_SCL : QPD_WPE2)
+                                : NS == 2 ? (KIND == K_SCL_LUT && !PFX ? QPD_WPE2_SCL : KIND == K_FASTSCL_LUT ? QPD_WPE2_FSCL : QPD_WPE2)
                                 : KIND == K_FASTSCL_LUT ? QPD_WPE_FSCL : QPD_WPE1) void lut_fast_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
                                                                uint8_t *__restrict__ out,
                                                                const MOp *__restrict__ ops) {
@@ -1647,7 +1903,10 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
     int *const sel_all = (int *)(lds_dyn + NS * P.lds_rows * 64);
     // list kinds at two frame sets: the f / g ops' byte tables (stage_tab), 768 B after
     // the selection scratch, and the folded descents (MF_FF)
-    constexpr bool kLdsTab = kList && NS >= 2;
+#ifndef QPD_EXP_NO_LDSTAB
+#define QPD_EXP_NO_LDSTAB 0  // A/B: the f / g lookups by ds_bpermute from the table register (no byte tables)
+#endif
+    constexpr bool kLdsTab = kList && NS >= 2 && !QPD_EXP_NO_LDSTAB;
     uint8_t *const tb = (uint8_t *)(sel_all + NS * kSelInts);
     Mem Mv[NS];
     {
@@ -1928,12 +2187,29 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                   // the sets one after the other, one copy of the code: set s runs in
                   // stv[0] (the sets' states rotate; back in place after NS steps) --
                   // the special nodes' code is not in the instruction cache twice
+                  if constexpr (KIND == K_FASTSCL_LUT && L8) {
+                    if (op.type == OP_R0 || op.type == OP_REP) {
+                        r0rep_multi(P, Mv, op, stv, sel_all, sstride, gl, gbase, lane);
+                        break;
+                    }
+                    if (op.type == OP_R1 && (op.cnt <= stl::kThreshold || (fl & MF_R1_LDS))) {
+                        r1_multi(P, Mv, op, stv, sel_all, sstride, gl, gbase, lane, lds_dyn);
+                        break;
+                    }
+                  }
+#if QPD_SPEC_ROT
 #pragma unroll 1
                   for (int s = 0; s < NS; ++s) {
                     special_op<kList, L8, R1L>(P, Mv[0].set(s), op, stv[0], sel_all + sstride * s, NS * sstride, gl, gbase,
                                                L, lane, lds_dyn);
                     rotate_sets(stv);
                   }
+#else
+#pragma unroll
+                  for (int s = 0; s < NS; ++s)
+                    special_op<kList, L8, R1L>(P, Mv[s], op, stv[s], sel_all + sstride * s, NS * sstride, gl, gbase, L, lane,
+                                               lds_dyn);
+#endif
                   break;
                 }
             }

@@ -156,52 +156,79 @@ def _run_point_all(step_fn, K, ebn0_db, batch, max_blocks, world, rank, group, c
 
 
 def run_point(generate, decode, K: int, ebn0_db: float, batch: int, max_blocks: int, stop_blkerrs: int | None = 1000,
-              A: int | None = None, group=None, count_device="cpu", gen_decode=None) -> PointResult:
+              A: int | None = None, group=None, count_device="cpu", gen_decode=None, shard=None,
+              virtual_world: int = 1) -> PointResult:
     """Run one Eb/N0 point.  ``generate(frame0, B) -> (msg, sym)`` and
     ``decode(sym) -> bits`` are this rank's frame source and decoder, or
     ``gen_decode(frame0, B) -> (msg, bits)`` does both in one call
     (GpuFrames.decode_frames); ``group`` is a torch.distributed process group
     (None = single process).  ``stop_blkerrs=None``: no early stop (every
-    frame up to max_blocks)."""
+    frame up to max_blocks).
+
+    Without a group, two ways to run the sharding of a ``world``-rank job in
+    one process (tests of config C5's 8-rank split on one device):
+    ``shard=(rank, world)`` (no early stop only) returns rank ``rank``'s
+    counters alone -- the ranks' results summed are the job's, which is what
+    the end-of-point all-reduce computes; ``virtual_world=W`` runs the W
+    ranks' slices of every step in lock step, combining them as the per-step
+    all-reduce / all-gather would (the stop rule's crossing may then fall in
+    any rank's slice)."""
     import torch
     import torch.distributed as dist
 
     A = K if A is None else A
     world = dist.get_world_size(group) if group is not None else 1
     rank = dist.get_rank(group) if group is not None else 0
+    if shard is not None:
+        assert group is None and stop_blkerrs is None, "shard=(rank, world): no group, no early stop"
+        rank, world = shard
     step_fn = _step_fn(generate, decode, gen_decode)
     if stop_blkerrs is None:
         counted = (lambda lo, n, acc: gen_decode(lo, n, counts=acc)) if gen_decode is not None else None
-        return _run_point_all(step_fn, K, ebn0_db, batch, max_blocks, world, rank, group, count_device, counted)
+        res = _run_point_all(step_fn, K, ebn0_db, batch, max_blocks, world, rank, group, count_device, counted)
+        if shard is not None:  # this rank's frames only
+            n = sum(max(0, min((rank + 1) * batch, min(world * batch, max_blocks - f0)) -
+                       min(rank * batch, min(world * batch, max_blocks - f0)))
+                    for f0 in range(0, max_blocks, world * batch))
+            res.frames_decoded = n
+        return res
+    if virtual_world > 1:
+        assert group is None, "virtual_world: no group"
+        world = virtual_world
+    vranks = list(range(world)) if virtual_world > 1 else [rank]
+
+    def local_step(f0, step, r):
+        lo = f0 + min(r * batch, step)
+        hi = f0 + min((r + 1) * batch, step)
+        if hi > lo:
+            msg, bits = step_fn(lo, hi - lo)
+            e = _frame_errors(bits, msg)
+            e_t = e if isinstance(e, torch.Tensor) else torch.from_numpy(e)
+            return e_t.to(count_device)
+        return torch.zeros(0, dtype=torch.int64, device=count_device)
+
     bit_errs = blk_errs = 0
     blocks = 0
     f0 = 0
     while f0 < max_blocks:
         step = min(world * batch, max_blocks - f0)
-        lo = f0 + min(rank * batch, step)
-        hi = f0 + min((rank + 1) * batch, step)
-        if hi > lo:
-            msg, bits = step_fn(lo, hi - lo)
-            e = _frame_errors(bits, msg)
-            e_t = e if isinstance(e, torch.Tensor) else torch.from_numpy(e)
-            e_t = e_t.to(count_device)
-            local = torch.stack([e_t.sum(), (e_t > 0).sum()]).to(torch.int64)
-        else:
-            e_t = torch.zeros(0, dtype=torch.int64, device=count_device)
-            local = torch.zeros(2, dtype=torch.int64, device=count_device)
-        tot = local.clone()
+        e_all = [local_step(f0, step, r) for r in vranks]
+        tot = sum(torch.stack([e.sum(), (e > 0).sum()]).to(torch.int64) for e in e_all)
         if group is not None:
             dist.all_reduce(tot, group=group)
         step_bits, step_blks = (int(x) for x in tot.tolist())
         if blk_errs + step_blks > stop_blkerrs:
             # locate the frame that crosses the threshold: gather per-frame counts in global order
-            pad = torch.zeros(batch, dtype=torch.int64, device=count_device)
-            pad[: e_t.numel()] = e_t
+            pads = []
+            for e_t in e_all:
+                pad = torch.zeros(batch, dtype=torch.int64, device=count_device)
+                pad[: e_t.numel()] = e_t
+                pads.append(pad)
             if group is not None:
-                parts = [torch.zeros_like(pad) for _ in range(world)]
-                dist.all_gather(parts, pad, group=group)
+                parts = [torch.zeros_like(pads[0]) for _ in range(world)]
+                dist.all_gather(parts, pads[0], group=group)
             else:
-                parts = [pad]
+                parts = pads
             per = np.concatenate([parts[r].cpu().numpy()[: max(0, min((r + 1) * batch, step) - min(r * batch, step))]
                                   for r in range(world)])
             for i, ef in enumerate(per):

@@ -95,6 +95,38 @@ def test_distributed_shards_give_identical_counts(world, batch):
         assert res[r] == want
 
 
+@pytest.mark.parametrize("world,batch,max_blocks", [(8, 16, 1000), (8, 100, 1000), (3, 7, 250), (8, 1, 20)])
+def test_shard_counters_sum_to_one_shot(world, batch, max_blocks):
+    """No early stop (config C5's MaxBlock branch): the `world` ranks' shards
+    run one after the other (shard=(rank, world)) sum to the one-shot counters,
+    as the end-of-point all-reduce does, and cover every frame once."""
+    want = driver_loop(errors_of(max_blocks), K, K, max_blocks, 10 ** 9)
+    parts = [MC.run_point(synthetic_source, lambda s: s, K, 1.0, batch, max_blocks, None, shard=(r, world))
+             for r in range(world)]
+    assert sum(p.bit_errors for p in parts) == want[2]
+    assert sum(p.block_errors for p in parts) == want[3]
+    assert sum(p.frames_decoded for p in parts) == max_blocks
+
+
+@pytest.mark.parametrize("world,batch,max_blocks,stop", [(8, 16, 2000, 40), (8, 5, 600, 25), (3, 9, 600, 25),
+                                                         (8, 64, 300, 10 ** 6)])
+def test_virtual_world_matches_driver_loop(world, batch, max_blocks, stop):
+    """The ranks' slices of every step in lock step (virtual_world): the
+    driver's counters and stop block, wherever the crossing frame falls."""
+    want = driver_loop(errors_of(max_blocks), K, K, max_blocks, stop)
+    got = MC.run_point(synthetic_source, lambda s: s, K, 1.0, batch, max_blocks, stop, virtual_world=world)
+    assert (got.ber, got.bler, got.bit_errors, got.block_errors, got.blocks, got.stopped_early) == want
+
+
+def test_virtual_world_crossing_outside_rank0():
+    """A case whose stop crossing lies in a slice other than rank 0's."""
+    world, batch, max_blocks, stop = 8, 16, 2000, 40
+    want = driver_loop(errors_of(max_blocks), K, K, max_blocks, stop)
+    assert want[5] and (want[4] % (world * batch)) // batch != 0  # the crossing block's rank
+    got = MC.run_point(synthetic_source, lambda s: s, K, 1.0, batch, max_blocks, stop, virtual_world=world)
+    assert got.blocks == want[4]
+
+
 def test_mc_ref_philox_known_answer():
     """Philox4x32-10 known-answer vector (Random123 kat_vectors: counter=0, key=0)."""
     from mc_ref import philox
