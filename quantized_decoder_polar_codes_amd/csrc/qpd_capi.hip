@@ -445,6 +445,19 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
         if (kind == QPD_FASTSCL_LUT && OP_R0 + t == OP_R1 && m.cnt <= 32) {
             m.tab = (int)r1tab.size();  // rank-key table of this node
             r1_rank_table(r1tab, vcl, N, v, d, node);
+            if ((m.flags & MF_VUNI) && !getenv("QPD_NO_R1RK")) {  // one row: the symbols' ranks (< 16) and signs in the record
+                uint64_t rk = 0;
+                uint32_t sg = 0;
+                for (int sy = 0; sy < v; ++sy) {
+                    const uint16_t e = r1tab[m.tab + sy];  // element 0's entry = every element's
+                    rk |= (uint64_t)(e >> 1) << (4 * sy);
+                    sg |= (uint32_t)(e & 1) << sy;
+                }
+                m.flags |= MF_R1_RK;
+                m.r_row = (int32_t)(uint32_t)rk;
+                m.tab2 = (int32_t)(uint32_t)(rk >> 32);
+                m.pad1 = (int32_t)sg;
+            }
             // > 16 elements: std::sort's introsort runs on 16-bit entries in the
             // free LDS tail of the wave (the sets' rows of depths > d + their
             // selection scratch; build_fast pads the LDS rows to make room)
@@ -483,7 +496,18 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
             return bot3_plain(kind, node_type, n, d + 1, c) ||
                    (Ly.botx && bot3_mixed(kind, node_type, vcl, N, n, v, c, &t0));
         };
-        const bool fuse = Ly.bfuse && d == n - 4 && d >= 2 && bot3_able(2 * node) && bot3_able(2 * node + 1);
+        // FastSCL-LUT (L = 8): a size-8 special child takes this node's f / g and combine too
+        // (MF_SFG / MF_SGG / MF_SCOMB: r0rep_multi, r1_multi in qpd_fast.hip); R1 only with its
+        // ranks in the op record (MF_R1_RK: the record's tab field then holds this node's table)
+        auto spec8_able = [&](int c) {
+            const int cp = (1 << (d + 1)) + c - 1, ts = special_of(kind, node_type, cp);
+            if (!Ly.botx || ts < 0 || getenv("QPD_NO_SFOLD")) return false;
+            return OP_R0 + ts != OP_R1 ||
+                   (v <= 16 && quanta_uniform(vcl, N, v, d + 1, c) && !getenv("QPD_NO_VUNI") && !getenv("QPD_NO_R1RK"));
+        };
+        const bool fuse = Ly.bfuse && d == n - 4 && d >= 2 && (bot3_able(2 * node) || spec8_able(2 * node)) &&
+                          (bot3_able(2 * node + 1) || spec8_able(2 * node + 1));
+        auto spec_child = [&](int c) { return !bot3_able(c); };  // (under `fuse`: a size-8 special child)
         for (int side = 0; side < 2; ++side) {
             MOp m = base(side ? OP_G : OP_F);
             m.cnt = N >> (d + 1);
@@ -501,6 +525,22 @@ void fast_ops(std::vector<qpd::MOp> &out, const FastLayout &Ly, int kind, int N,
             if (Ly.pre && d == 0) {  // root in pre-mode: f(y) comes from the pre-pass row, g(y, u) by selects
                 m.flags = (m.flags & ~MF_CHAN) | MF_PRE | MF_GSEL;
                 m.src_row = N >> 4;  // g(y, 0) words; g(y, 1) follow
+            }
+            if (fuse && spec_child(2 * node + side)) {
+                const size_t at = out.size();
+                fast_ops(out, Ly, kind, N, n, v, frozen, node_type, vcl, r1tab, d + 1, 2 * node + side);
+                MOp &b = out[at];  // the child's special op: this node's f / g (and combine) folded in
+                b.flags = (b.flags & ~MF_SRC_LDS) | (m.flags & MF_SRC_LDS) | MF_SFG;
+                b.src_row = m.src_row;
+                b.sh_src = m.sh_src;
+                b.tab = m.tab;
+                if (side) {
+                    b.flags = (b.flags & ~(MF_DST_LDS | MF_TO_R)) | MF_SGG | MF_SCOMB | (m.flags & MF_U_LDS);
+                    b.u_row = m.u_row;  // U[n-3] of the left child: g's u bits, then the combine's left half
+                    b.sh_u = m.sh_u;
+                    finish_node(b);  // this node's destination
+                }
+                continue;
             }
             if (fuse) {
                 const size_t at = out.size();
@@ -643,12 +683,14 @@ void place_syncs(std::vector<qpd::MOp> &ops, bool list) {
             default: break;
         }
         const bool src_glb = !(m.flags & (MF_SRC_LDS | MF_CHAN | MF_PRE));
-        const bool u_glb = ((m.type == OP_G || m.type == OP_COMB || m.type == OP_LEAF_R ||
+        const bool spec_u = m.type >= OP_R0 && m.type <= OP_SPC && (m.flags & (MF_SGG | MF_SCOMB));
+        const bool u_glb = ((m.type == OP_G || m.type == OP_COMB || m.type == OP_LEAF_R || spec_u ||
                              (m.type == OP_BOT3 && (m.flags & (MF_BG | MF_BCOMB)))) &&
                             !(m.flags & MF_U_LDS)) ||
                            (m.type == OP_BOT3 && (m.flags & MF_BC2) && !(m.flags & MF_BC2_ULDS));
-        const bool late_u = m.type == OP_BOT3 && forks &&
-                            (((m.flags & MF_BCOMB) && !(m.flags & MF_U_LDS)) || ((m.flags & MF_BC2) && !(m.flags & MF_BC2_ULDS)));
+        const bool late_u = (m.type == OP_BOT3 && forks &&
+                             (((m.flags & MF_BCOMB) && !(m.flags & MF_U_LDS)) || ((m.flags & MF_BC2) && !(m.flags & MF_BC2_ULDS)))) ||
+                            (forks && (m.flags & MF_SCOMB) && spec_u && !(m.flags & MF_U_LDS));
         if ((exposed && (src_glb || u_glb)) || (late_u && dirty)) {
             m.flags |= MF_SYNC;
             exposed = dirty = false;
@@ -998,6 +1040,7 @@ bool compact_pointer_fields(const std::vector<std::vector<qpd::MOp> *> &lists) {
                 break;
             default:  // special nodes
                 fn(0, m.sh_src);
+                if (fl & (MF_SGG | MF_SCOMB)) fn(1, m.sh_u);
                 if (!(fl & MF_TO_R)) fn(1, m.sh_dst);
                 break;
         }
@@ -1156,7 +1199,8 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
             if (!(m.flags & (MF_CHAN | MF_PRE))) mark(m.src_row);
             mark(m.dst_row);
             if (m.type == OP_G || m.type == OP_LEAF_R || m.type == OP_COMB ||
-                (m.type == OP_BOT3 && (m.flags & (MF_BG | MF_BCOMB))))
+                (m.type == OP_BOT3 && (m.flags & (MF_BG | MF_BCOMB))) ||
+                (m.type >= OP_R0 && m.type <= OP_SPC && (m.flags & (MF_SGG | MF_SCOMB))))
                 mark(m.u_row);
             if (m.type == OP_COMB) mark(m.r_row);
         }

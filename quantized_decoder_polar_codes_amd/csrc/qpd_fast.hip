@@ -68,6 +68,12 @@ enum MopFlag : int32_t {
     MF_BC2_DLDS = 8388608,  //   ... the result row in LDS
     MF_BC2_TOR = 16777216,  //   ... the grandparent is a right child (R row: no pointer update)
     MF_BOTX = 33554432,     // BOT3 of a subtree with FastSCL special nodes of size 4 / 2 (botx_op)
+    MF_R1_RK = 67108864,    // R1 with one quanta row: symbol s's rank in bits 4s..4s+3 of r_row | tab2 << 32 and
+                            //   its sign in bit s of pad1 (r1_prep: no per-element rank lookups)
+    MF_SFG = 134217728,     // size-8 special node (FastSCL-LUT, L = 8) that computes its 8 symbols as f of its
+                            //   depth n-4 parent's 16 (src = S[n-4], the parent's table at tab): no F op
+    MF_SGG = 268435456,     //   ... as g of them, u = the left sibling's U[n-3] at u_row (sh_u): no G op
+    MF_SCOMB = 536870912,   //   ... and runs the parent's combine with that U[n-3] (dst = the parent's): no COMB
 };
 
 struct MOp {
@@ -630,6 +636,8 @@ __device__ __forceinline__ Pre fetch_pre(const FastPlan &P, const MOp &op, int l
                                       : tab_ld(P.f_tab, op.tab2 * QPD_EXP_TABMUL, lane & 31);
     }
     if (op.type == OP_LEAF_L || op.type == OP_LEAF_R) p.V = P.vcl[op.vrow + vlane];
+    if (op.type >= OP_R0 && op.type <= OP_SPC && (op.flags & MF_SFG))  // the folded parent's table (tab)
+        p.T2 = (op.flags & MF_SGG) ? tab_ld(P.g_tab, op.tab, lane) : tab_ld(P.f_tab, op.tab, lane & 31);
     return p;
 }
 
@@ -1386,32 +1394,62 @@ __device__ __forceinline__ uint32_t r1_layers(Path &st, int *sel, int sj, int gl
     return temp < 32 ? word & ((1u << temp) - 1u) : word;
 }
 
+// Word w of a special node's symbols: its S[d] row, or (MF_SFG, size-8 nodes)
+// f / g (MF_SGG, u = the left sibling's U[d] through usrc) of its depth d-1
+// parent's two words, with the parent's table T2 (staged as bytes at tb: LT).
+template <bool LT>
+__device__ __forceinline__ uint32_t spec_in(const Mem &M, const MOp &op, int src, int usrc, int w, uint32_t T2,
+                                            const uint8_t *tb) {
+    const bool sl = op.flags & MF_SRC_LDS;
+    if (!(op.flags & MF_SFG)) return M.ld(sl, op.src_row + w, src);
+    const uint32_t a = M.ld(sl, op.src_row, src), b = M.ld(sl, op.src_row + 1, src);
+    const uint32_t ub = (op.flags & MF_SGG) ? M.ld(op.flags & MF_U_LDS, op.u_row, usrc) : 0u;
+    return LT ? lut_lds<8, true>(tb, a, b, ub) : lut_vec<8>(T2, a, b, ub);  // (f: ub = 0, entries < 256)
+}
+
+// A special node's result word(s) `res` to its destination; MF_SCOMB (size 8):
+// the parent's combine with the left sibling's U[d] (through the path's
+// pointer after the node's forks, as the COMB op would read it) instead, to
+// the parent's destination (utils.cpp:62-67).
+template <class Path>
+__device__ __forceinline__ void spec_out(const Mem &M, const MOp &op, Path &st, int gbase, int gl, int lane, int w,
+                                         uint32_t res) {
+    if (op.flags & MF_SCOMB)
+        res = ((M.ld(op.flags & MF_U_LDS, op.u_row, gbase + pfield(st.U(), op.sh_u)) & 0xFFu) ^ res) | (res << 8);
+    M.st(op.flags & MF_DST_LDS, op.dst_row + w, lane, res);
+}
+
 // The argsort half of an R1 node of <= 32 elements (:100-116) for one set:
 // the m smallest |l| in std::sort's order, packed for r1_layers.
 struct R1Prep {
     uint32_t ordp0, ordp1, symp, hw;
 };
 
-template <class Path>
-__device__ __forceinline__ R1Prep r1_prep(const FastPlan &P, const Mem &M, const MOp &op, const Path &st, int gbase, int L,
-                                          int lane, int temp, uint32_t *lds_wave) {
+template <bool LT = false, class Path>
+__device__ __forceinline__ R1Prep r1_prep(const FastPlan &P, const Mem &M, const MOp &op, Path st, int gbase, int L,
+                                          int lane, int temp, uint32_t *lds_wave, uint32_t T2 = 0u,
+                                          const uint8_t *tb = nullptr) {
     const int src = gbase + pfield(st.ps, op.sh_src);
-    const bool sl = op.flags & MF_SRC_LDS;
     const int v = P.v;
     const int m = (L - 1) < temp ? (L - 1) : temp;
     const uint16_t *rk = P.r1_rank + op.tab;
     const double *vq = P.vcl + (size_t)op.vrow * v;
     // MF_VUNI: one quanta row and one rank row for all elements, in registers
-    const bool uni = op.flags & MF_VUNI;
+    const bool uni = op.flags & MF_VUNI, rku = op.flags & MF_R1_RK;
     const int s16 = lane & 15;
-    const uint32_t rrow = uni && s16 < v ? (uint32_t)rk[s16] : 0u;
+    const uint32_t rrow = uni && !rku && s16 < v ? (uint32_t)rk[s16] : 0u;
     const double vrow = uni && s16 < v ? vq[s16] : 0.0;
+    // rank << 1 | sign of element j's symbol: from the op record's words (MF_R1_RK), the node's
+    // one rank row in a register (MF_VUNI), or the per-element rank table
+    const uint64_t RK = ((uint64_t)(uint32_t)op.tab2 << 32) | (uint32_t)op.r_row;
     auto rank_of = [&](int j, uint32_t sym) -> uint32_t {
+        if (rku) return ((uint32_t)(RK >> (4 * sym)) & 15u) << 1 | (((uint32_t)op.pad1 >> sym) & 1u);
         return uni ? (uint32_t)lane_read((int)rrow, (int)sym) : (uint32_t)rk[j * v + sym];
     };
     uint32_t W[4], hw = 0;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) W[w] = (8 * w < temp) ? M.ld(sl, op.src_row + w, src) : 0u;
+    for (int w = 0; w < 4; ++w)
+        W[w] = (8 * w < temp) ? spec_in<LT>(M, op, src, gbase + pfield(st.U(), op.sh_u), w, T2, tb) : 0u;
     int ord[kMaxM];
 #pragma unroll
     for (int q = 0; q < kMaxM; ++q) ord[q] = 0;
@@ -1468,10 +1506,48 @@ __device__ __forceinline__ R1Prep r1_prep(const FastPlan &P, const Mem &M, const
                 seq.set(j, (int)(((e >> 1) << 5) | (uint32_t)j));
             }
         }
-        stl::sort_small_prefix(seq, 0, temp, m);  // only ord[0, m) is read
+        if (rku) {
+            // the partitions in LDS, then the m smallest of the block [0, end) by (rank, position):
+            // what the final insertion sort's first m outputs are (stl::partition_prefix), by
+            // packed 16-bit min trees over rank << 10 | position << 5 | element (ranks < 16)
+            const int end = stl::partition_prefix(seq, 0, temp, m);
+            typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+            u16x2 ep[16];
 #pragma unroll
-        for (int q = 0; q < kMaxM; ++q)
-            if (q < m) ord[q] = seq.get(q) & 31;
+            for (int i = 0; i < 16; ++i) {
+                const uint32_t d = 2 * i < temp ? *(const uint32_t *)(seq.lane0 + i * seq.hs) : 0u;  // entries 2i, 2i + 1
+                const uint32_t e0 = d & 0xffffu, e1 = d >> 16;
+                const uint32_t lo = 2 * i < end ? ((e0 >> 5) << 10) | ((uint32_t)(2 * i) << 5) | (e0 & 31u) : 0xffffu;
+                const uint32_t hi = 2 * i + 1 < end ? ((e1 >> 5) << 10) | ((uint32_t)(2 * i + 1) << 5) | (e1 & 31u) : 0xffffu;
+                ep[i] = __builtin_bit_cast(u16x2, lo | (hi << 16));
+            }
+#pragma unroll
+            for (int q = 0; q < kMaxM; ++q) {
+                if (q < m) {
+                    u16x2 a[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) a[i] = __builtin_elementwise_min(ep[2 * i], ep[2 * i + 1]);
+#pragma unroll
+                    for (int w = 4; w >= 1; w >>= 1)
+#pragma unroll
+                        for (int i = 0; i < w; ++i) a[i] = __builtin_elementwise_min(a[i], a[i + w]);
+                    const uint32_t mn = a[0].x < a[0].y ? a[0].x : a[0].y;
+                    ord[q] = (int)(mn & 31u);
+                    const u16x2 mm = {(unsigned short)mn, (unsigned short)mn};
+                    const u16x2 one = {1, 1}, zero = {0, 0};
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const u16x2 dd = ep[i] - mm;
+                        ep[i] = ep[i] | (zero - (__builtin_elementwise_min(dd, one) ^ one));  // taken -> 0xFFFF
+                    }
+                }
+            }
+        } else {
+            stl::sort_small_prefix(seq, 0, temp, m);  // only ord[0, m) is read
+#pragma unroll
+            for (int q = 0; q < kMaxM; ++q)
+                if (q < m) ord[q] = seq.get(q) & 31;
+        }
     }
     R1Prep r{0u, 0u, 0u, hw};
 #pragma unroll
@@ -1506,18 +1582,21 @@ __device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const 
 // R1 nodes of <= 32 elements with L = 8 for all the wave's frame sets: the
 // argsorts set by set, then the layers of the sets interleaved (their fork
 // chains overlap), each set stopping at its first identity layer (r1_layers).
-template <int NS, class Path>
+template <bool LT, int NS, class Path>
 __device__ __forceinline__ void r1_multi(const FastPlan &P, const Mem (&Mv)[NS], const MOp &op, Path (&st)[NS], int *sel_all,
-                                         int sstride, int gl, int gbase, int lane, uint32_t *lds_wave) {
+                                         int sstride, int gl, int gbase, int lane, uint32_t *lds_wave, uint32_t T2,
+                                         uint8_t *tb) {
     const int temp = op.cnt, v = P.v;
     const int m = kMaxM < temp ? kMaxM : temp;  // L = 8
     const double *vq = P.vcl + (size_t)op.vrow * v;
     const bool uni = op.flags & MF_VUNI;
     const double vrow = uni && (lane & 15) < v ? vq[lane & 15] : 0.0;
+    if constexpr (LT)
+        if (op.flags & MF_SFG) stage_tab(tb, T2, (op.flags & MF_SGG) ? lane : (lane & 31));
     R1Prep pr[NS];
 #pragma unroll 1
     for (int s = 0; s < NS; ++s) {  // set s in slot 0 (rotate_sets)
-        pr[0] = r1_prep(P, Mv[0].set(s), op, st[0], gbase, 8, lane, temp, lds_wave);
+        pr[0] = r1_prep<LT>(P, Mv[0].set(s), op, st[0], gbase, 8, lane, temp, lds_wave, T2, tb);
         rotate_sets(st);
         rotate_sets(pr);
     }
@@ -1564,7 +1643,7 @@ __device__ __forceinline__ void r1_multi(const FastPlan &P, const Mem (&Mv)[NS],
     for (int s = 0; s < NS; ++s) {
         uint32_t word = (uint32_t)lane_read((int)pr[s].hw, gbase + origin[s]) ^ flips[s];
         if (temp < 32) word &= (1u << temp) - 1u;
-        Mv[s].st(op.flags & MF_DST_LDS, op.dst_row, lane, word);
+        spec_out(Mv[s], op, st[s], gbase, gl, lane, 0, word);
         if (!(op.flags & MF_TO_R)) st[s].U() = pset(st[s].U(), op.sh_dst, gl);
     }
 }
@@ -1572,9 +1651,9 @@ __device__ __forceinline__ void r1_multi(const FastPlan &P, const Mem (&Mv)[NS],
 // R0 / REP nodes with L = 8 for all the wave's frame sets, interleaved element
 // by element (their sums are dependent fp64 chains in the reference's order,
 // H5; the sets' chains overlap).
-template <int NS, class Path>
+template <bool LT, int NS, class Path>
 __device__ __forceinline__ void r0rep_multi(const FastPlan &P, const Mem (&Mv)[NS], const MOp &op, Path (&st)[NS], int *sel_all,
-                                            int sstride, int gl, int gbase, int lane) {
+                                            int sstride, int gl, int gbase, int lane, uint32_t T2, uint8_t *tb) {
     const int fl = op.flags, temp = op.cnt, v = P.v;
     const bool rep = op.type == OP_REP, sl = fl & MF_SRC_LDS, dl = fl & MF_DST_LDS;
     const double *vq = P.vcl + (size_t)op.vrow * v;  // row d-1, position temp*node
@@ -1588,11 +1667,13 @@ __device__ __forceinline__ void r0rep_multi(const FastPlan &P, const Mem (&Mv)[N
         kk[s] = kf[s] = st[s].pm;
     }
     const int n8 = (temp + 7) >> 3;
+    if constexpr (LT)
+        if (fl & MF_SFG) stage_tab(tb, T2, (fl & MF_SGG) ? lane : (lane & 31));
 #pragma unroll 1
     for (int w = 0; w < n8; ++w) {
         uint32_t word[NS];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) word[s] = Mv[s].ld(sl, op.src_row + w, src[s]);
+        for (int s = 0; s < NS; ++s) word[s] = spec_in<LT>(Mv[s], op, src[s], gbase + pfield(st[s].U(), op.sh_u), w, T2, tb);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             if (8 * w + i >= temp) break;
@@ -1619,7 +1700,7 @@ __device__ __forceinline__ void r0rep_multi(const FastPlan &P, const Mem (&Mv)[N
             st[s].move(p);
             fill = sx.upper ? 0xffffffffu : 0u;
         }
-        for (int w = 0; w < nwo; ++w) Mv[s].st(dl, op.dst_row + w, lane, fill & m);
+        for (int w = 0; w < nwo; ++w) spec_out(Mv[s], op, st[s], gbase, gl, lane, w, fill & m);
         if (!(fl & MF_TO_R)) st[s].U() = pset(st[s].U(), op.sh_dst, gl);
     }
 }
@@ -2189,11 +2270,11 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                   // the special nodes' code is not in the instruction cache twice
                   if constexpr (KIND == K_FASTSCL_LUT && L8) {
                     if (op.type == OP_R0 || op.type == OP_REP) {
-                        r0rep_multi(P, Mv, op, stv, sel_all, sstride, gl, gbase, lane);
+                        r0rep_multi<kLdsTab>(P, Mv, op, stv, sel_all, sstride, gl, gbase, lane, cur.T2, tb);
                         break;
                     }
                     if (op.type == OP_R1 && (op.cnt <= stl::kThreshold || (fl & MF_R1_LDS))) {
-                        r1_multi(P, Mv, op, stv, sel_all, sstride, gl, gbase, lane, lds_dyn);
+                        r1_multi<kLdsTab>(P, Mv, op, stv, sel_all, sstride, gl, gbase, lane, lds_dyn, cur.T2, tb);
                         break;
                     }
                   }

@@ -231,9 +231,15 @@ QPD_HD void sort_small(Seq &s, int first, int last) {
 // with c - first >= m is known, the order of [first, c) is final-insertion-sort
 // of [first, c) alone: the right part's partitioning and its insertions are
 // skipped.  Positions >= c of the array are left unsorted.
+//
+// partition_prefix runs the partitioning part and returns that end; the final
+// insertion sort of [first, end) is then a STABLE sort of the block as the
+// partitions left it (insertion_sort and unguarded_linear_insert move an
+// element only past strictly greater keys), so its first m outputs are the m
+// smallest entries by (key, position in the block) -- which the device finds
+// with packed min trees instead of the O(n^2) insertions (r1_prep).
 template <class Seq>
-QPD_HD void sort_small_prefix(Seq &s, int first, int last, int m) {
-    if (first == last) return;
+QPD_HD int partition_prefix(Seq &s, int first, int last, int m) {
     int f = first, l = last, dl = lg(last - first) * 2, end = last;
     while (l - f > kThreshold) {
         if (dl == 0) {
@@ -252,7 +258,13 @@ QPD_HD void sort_small_prefix(Seq &s, int first, int last, int m) {
             l = cut;
         }
     }
-    final_insertion_sort(s, first, end);
+    return end;
+}
+
+template <class Seq>
+QPD_HD void sort_small_prefix(Seq &s, int first, int last, int m) {
+    if (first == last) return;
+    final_insertion_sort(s, first, partition_prefix(s, first, last, m));
 }
 
 template <class Seq>

@@ -52,6 +52,17 @@ int main(int argc, char **argv) {
                 const int k = std::min(m, n);
                 if (!std::equal(a.begin(), a.begin() + k, e.begin()) && ++bad < 5)
                     printf("sort_small_prefix mismatch n=%d m=%d distinct=%d\n", n, m, distinct);
+                // partition_prefix + the m smallest by (key, block position): the device's selection
+                std::vector<int> g(n);
+                for (int i = 0; i < n; ++i) g[i] = i;
+                VecSeq s4{g, key};
+                const int end = n ? qpd::stl::partition_prefix(s4, 0, n, m) : 0;
+                std::vector<int> pos(end);
+                for (int i = 0; i < end; ++i) pos[i] = i;
+                std::stable_sort(pos.begin(), pos.end(), [&](int p, int q) { return key[g[p]] < key[g[q]]; });
+                bool ok = end >= k;
+                for (int q = 0; q < k && ok; ++q) ok = g[pos[q]] == a[q];
+                if (!ok && ++bad < 5) printf("partition_prefix selection mismatch n=%d m=%d distinct=%d\n", n, m, distinct);
             }
         }
     }

@@ -64,6 +64,39 @@ def test_botx_random_codes(N, seed, qpd, oracle_mod, monkeypatch):
     assert_frames_equal(b.decode_batch(sym), want, b, f"nobotx-{N}-{seed}")
 
 
+@pytest.mark.parametrize("N", [64, 256])
+@pytest.mark.parametrize("seed", range(4))
+def test_special_folds_random_codes(N, seed, qpd, oracle_mod, monkeypatch):
+    """Size-8 special nodes that take their parent's f / g and combine
+    (MF_SFG / MF_SGG / MF_SCOMB) = the unfolded schedule (QPD_NO_SFOLD=1) = the
+    oracle, on codes with every mix of size-8 special and BOT3 siblings."""
+    from quantized_decoder_polar_codes_amd import lut as LU
+
+    fm, nt, K = _random_code(N, 300 * N + seed)
+    p = LU.random_luts(N, 16, seed=seed + 50, distinct_mags=3, node_rows=True)
+    sym = np.random.default_rng(seed).integers(0, 16, size=(300, N), dtype=np.int32)
+    monkeypatch.delenv("QPD_NO_SFOLD", raising=False)
+    a = qpd.from_packed("FastSCL-LUT", p, K, fm, L=8, node_type=nt, engine="fast")
+    monkeypatch.setenv("QPD_NO_SFOLD", "1")
+    b = qpd.from_packed("FastSCL-LUT", p, K, fm, L=8, node_type=nt, engine="fast")
+    monkeypatch.delenv("QPD_NO_SFOLD")
+    want = oracle_mod.decode_lut("FastSCL-LUT", p, K, 8, fm, sym, node_type=nt)
+    assert_frames_equal(a.decode_batch(sym), want, a, f"sfold-{N}-{seed}")
+    assert_frames_equal(b.decode_batch(sym), want, b, f"nosfold-{N}-{seed}")
+
+
+def test_special_folds_engage(qpd, monkeypatch):
+    """The bench code's 13 size-16 nodes with one size-8 special child lose their F / G / COMB ops
+    (39; a few more of the depth n-5 combines then fold into right BOT3s, MF_BC2)."""
+    import bench
+
+    wl = bench.workload(1024, 512, 8, "FastSCL-LUT", 0, 2.0)
+    monkeypatch.setenv("QPD_NO_SFOLD", "1")
+    b = qpd.from_packed("FastSCL-LUT", wl.packed, 512, wl.fm, L=8, node_type=wl.nt)
+    monkeypatch.delenv("QPD_NO_SFOLD")
+    assert wl.dec.info()["num_ops"] <= b.info()["num_ops"] - 39
+
+
 def test_botx_engages_on_random_codes(qpd, monkeypatch):
     """The random codes above do take the fused op (fewer ops than unfused)."""
     from quantized_decoder_polar_codes_amd import lut as LU
@@ -83,6 +116,7 @@ def test_botx_needs_one_quanta_row(qpd, oracle_mod, monkeypatch):
 
     fm, nt, K = _random_code(128, 77)
     p = LU.random_luts(128, 16, seed=77, distinct_mags=3)
+    monkeypatch.setenv("QPD_NO_SFOLD", "1")  # (the special-node folds need no quanta row)
     a, b = _pair(qpd, monkeypatch, "FastSCL-LUT", p, K, fm, 8, nt)
     assert a.info()["num_ops"] == b.info()["num_ops"]
     sym = np.random.default_rng(77).integers(0, 16, size=(200, 128), dtype=np.int32)
