@@ -1335,6 +1335,76 @@ __device__ __forceinline__ void botx_op(const FastPlan &P, const Mem (&M)[NS], c
 // in the reference's sequential element order (H5).
 // ---------------------------------------------------------------------------
 
+__device__ __forceinline__ uint32_t lomask(int x) { return x >= 32 ? 0xffffffffu : ((1u << x) - 1u); }
+__device__ __forceinline__ uint32_t hibit(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }  // x != 0
+
+// stl::partition_prefix on an R1 array of 17..32 entries (keys < 16, MF_R1_RK),
+// each Hoare partition driven by bit masks instead of its scans' dependent
+// LDS reads: per round one pass over the array gives the positions whose key
+// is >= / <= the pivot's; a partition's i-th left stop is then the next such
+// position after the previous stop, or the previous right stop (whose
+// swapped-in entry stops the scan there), the right stops likewise, and only
+// the swaps touch LDS.  Returns `end` (partition_prefix); heap-sort fallbacks
+// (the depth limit, never on the bench code) run stl::heap_sort as the
+// reference does.
+template <class Seq>
+__device__ __forceinline__ int partition_prefix_masked(Seq &s, int temp, int m) {
+    int f = 0, l = temp, dl = 0, end = temp;
+    for (int t = temp; t > 1; t >>= 1) dl += 2;  // 2 * lg(temp)
+    bool live = l - f > stl::kThreshold;
+#pragma unroll 1
+    while (__builtin_amdgcn_ballot_w64(live)) {
+        if (live) {
+            if (dl == 0) {
+                stl::heap_sort(s, f, l);
+                live = false;
+            } else {
+                --dl;
+                stl::move_median_to_first(s, f, f + 1, f + (l - f) / 2, l - 1);
+            }
+        }
+        // ranks >= / <= the pivot's over the 32 positions (one read pass)
+        const uint32_t pv = (uint32_t)s.get(live ? f : 0) >> 5;
+        uint32_t GE = 0u, LE = 0u;
+#pragma unroll 4
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t d = 2 * i < temp ? *(const uint32_t *)(s.lane0 + i * s.hs) : 0u;
+            const uint32_t k0 = (d & 0xffffu) >> 5, k1 = d >> 21;
+            GE |= ((uint32_t)(k0 >= pv) << (2 * i)) | ((uint32_t)(k1 >= pv) << (2 * i + 1));
+            LE |= ((uint32_t)(k0 <= pv) << (2 * i)) | ((uint32_t)(k1 <= pv) << (2 * i + 1));
+        }
+        const uint32_t g0 = GE & lomask(l) & ~lomask(f + 1), e0 = LE & lomask(l) & ~lomask(f);
+        uint32_t a = g0 ? (uint32_t)__builtin_ctz(g0) : 32u, b = e0 ? hibit(e0) : 0u;
+        bool act = live && a < b;
+#pragma unroll 1
+        while (__builtin_amdgcn_ballot_w64(act)) {
+            if (act) {
+                const int ea = s.get((int)a), eb = s.get((int)b);
+                s.set((int)a, eb);
+                s.set((int)b, ea);
+                const uint32_t in = lomask((int)b) & ~lomask((int)a + 1);
+                const uint32_t g = GE & in, e = LE & in;
+                const uint32_t na = g ? (uint32_t)__builtin_ctz(g) : b, nb = e ? hibit(e) : a;
+                a = na;
+                b = nb;
+                act = a < b;
+            }
+        }
+        if (live) {
+            const int cut = (int)a;
+            if (cut >= m && cut < end) end = cut;
+            if (l - cut > stl::kThreshold) {
+                if (cut >= end) live = false;
+                else f = cut;
+            } else {
+                l = cut;
+            }
+            live = live && l - f > stl::kThreshold;
+        }
+    }
+    return end;
+}
+
 // LDS view of the R1 argsort array: 16-bit entries (rank << 5 | element),
 // entry p of this lane at row base + p/2, half p%2 of the lane's dword (rows
 // `hs` halfwords apart: the set-interleaved row stride, see Mem).
@@ -1510,7 +1580,7 @@ __device__ __forceinline__ R1Prep r1_prep(const FastPlan &P, const Mem &M, const
             // the partitions in LDS, then the m smallest of the block [0, end) by (rank, position):
             // what the final insertion sort's first m outputs are (stl::partition_prefix), by
             // packed 16-bit min trees over rank << 10 | position << 5 | element (ranks < 16)
-            const int end = stl::partition_prefix(seq, 0, temp, m);
+            const int end = QPD_EXP_FSCL & 128 ? stl::partition_prefix(seq, 0, temp, m) : partition_prefix_masked(seq, temp, m);
             typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
             u16x2 ep[16];
 #pragma unroll
@@ -1596,6 +1666,8 @@ __device__ __forceinline__ void r1_multi(const FastPlan &P, const Mem (&Mv)[NS],
     R1Prep pr[NS];
 #pragma unroll 1
     for (int s = 0; s < NS; ++s) {  // set s in slot 0 (rotate_sets)
+        if ((QPD_EXP_FSCL & 64) && temp > 16) pr[0] = R1Prep{0x1a418820u, 6u, 0u, 0u};  // (ord 0..6)
+        else
         pr[0] = r1_prep<LT>(P, Mv[0].set(s), op, st[0], gbase, 8, lane, temp, lds_wave, T2, tb);
         rotate_sets(st);
         rotate_sets(pr);
@@ -1610,7 +1682,7 @@ __device__ __forceinline__ void r1_multi(const FastPlan &P, const Mem (&Mv)[NS],
         done[s] = false;
     }
 #pragma unroll 1
-    for (int layer = 0; layer < m; ++layer) {
+    for (int layer = 0; layer < ((QPD_EXP_FSCL & 32) && temp > 16 ? 0 : m); ++layer) {
         double kf[NS];
         int own[NS];
         bool all = true;

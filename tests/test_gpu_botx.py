@@ -85,6 +85,26 @@ def test_special_folds_random_codes(N, seed, qpd, oracle_mod, monkeypatch):
     assert_frames_equal(b.decode_batch(sym), want, b, f"nosfold-{N}-{seed}")
 
 
+@pytest.mark.parametrize("N,K,mags", [(1024, 512, 2), (1024, 512, 3), (1024, 480, 2), (1024, 560, 4), (512, 300, 2)])
+def test_r1_bitplane_argsort(N, K, mags, qpd, oracle_mod):
+    """R1 nodes of 17..32 elements with one quanta row (MF_R1_RK): the argsort
+    replayed on bit planes in registers (r1_bitplane) on tie-heavy tables
+    (2-4 magnitudes: the partitions meet many equal keys) = the oracle."""
+    from quantized_decoder_polar_codes_amd import codes as C
+    from quantized_decoder_polar_codes_amd import lut as LU
+
+    _, mb, fm, _ = C.construct_pw(N, K)
+    nt = C.identify_nodes(N, mb).astype(np.int32)
+    sizes = [N >> d for d in range(int(np.log2(N))) for node in range(1 << d)
+             if nt[(1 << d) + node - 1] == 1]
+    assert any(16 < t <= 32 for t in sizes)
+    p = LU.random_luts(N, 16, seed=N + K + mags, distinct_mags=mags, node_rows=True)
+    sym = np.random.default_rng(K).integers(0, 16, size=(128, N), dtype=np.int32)
+    want = oracle_mod.decode_lut("FastSCL-LUT", p, K, 8, fm, sym, node_type=nt)
+    dec = qpd.from_packed("FastSCL-LUT", p, K, fm, L=8, node_type=nt, engine="fast")
+    assert_frames_equal(dec.decode_batch(sym), want, dec, f"r1-bitplane-{N}-{K}-{mags}")
+
+
 def test_special_folds_engage(qpd, monkeypatch):
     """The bench code's 13 size-16 nodes with one size-8 special child lose their F / G / COMB ops
     (39; a few more of the depth n-5 combines then fold into right BOT3s, MF_BC2)."""
