@@ -144,7 +144,8 @@ struct FastPlan {
 #endif
 #ifndef QPD_EXP_FSCL
 #define QPD_EXP_FSCL 0  // code-quality experiments (wrong results for those ops): 2 no special ops,
-                        // 4 no R1, 8 no R1 LDS introsort, 16 no REP
+                        // 4 no R1, 8 no R1 LDS introsort, 16 no REP, 128 old partition loop, 256 no special
+                        // ops at all, 512 no multi-set R0/REP, 1024 no multi-set R1
 #endif
 
 #ifndef QPD_SLAB_AUX
@@ -1124,6 +1125,9 @@ __device__ __forceinline__ void bx_spec_multi(Path (&st)[NS], uint32_t (&x)[NS][
         x[s][1] = (uint32_t)lane_read((int)x[s][1], p);
         return p;
     };
+#ifdef QPD_BXE
+    if (QPD_BXE & 1) return;
+#endif
     if (type != BX_R1) {  // R0 (:83-98) / REP (:169-213)
         double kk[NS], kf[NS];
 #pragma unroll
@@ -1150,6 +1154,9 @@ __device__ __forceinline__ void bx_spec_multi(Path (&st)[NS], uint32_t (&x)[NS][
         }
         return;
     }
+#ifdef QPD_BXE
+    if (QPD_BXE & 2) return;
+#endif
     // R1 (:100-166): per set r = ord | ranked symbols | decisions, as bx_spec
     uint32_t r[NS];
 #pragma unroll
@@ -1291,6 +1298,9 @@ __device__ __forceinline__ void botx_op(const FastPlan &P, const Mem (&M)[NS], c
             const uint32_t w1 = sub ? g_pair(cur.t1, (x[s][1] >> 25) & 3u, w2) : f_pair(cur.t1, 0u, w2);
             x[s][1] = (x[s][1] & ~(0xffu << 16)) | (w1 << 16);
         }
+#ifdef QPD_BXE
+        if (QPD_BXE & 4) continue;
+#endif
         if (t2 == BX_PLAIN) {
             bot_pair<true, true, false>(st, x, cur.tf, 0, cur.tg, cur.V, 0, fr >> (2 * k), gl, gbase, L, lane, sel, sstride, c);
         } else {
@@ -1368,7 +1378,7 @@ __device__ __forceinline__ int partition_prefix_masked(Seq &s, int temp, int m) 
         uint32_t GE = 0u, LE = 0u;
 #pragma unroll 4
         for (int i = 0; i < 16; ++i) {
-            const uint32_t d = 2 * i < temp ? *(const uint32_t *)(s.lane0 + i * s.hs) : 0u;
+            const uint32_t d = 2 * i < temp ? s.pair(i) : 0u;
             const uint32_t k0 = (d & 0xffffu) >> 5, k1 = d >> 21;
             GE |= ((uint32_t)(k0 >= pv) << (2 * i)) | ((uint32_t)(k1 >= pv) << (2 * i + 1));
             LE |= ((uint32_t)(k0 <= pv) << (2 * i)) | ((uint32_t)(k1 <= pv) << (2 * i + 1));
@@ -1411,6 +1421,12 @@ __device__ __forceinline__ int partition_prefix_masked(Seq &s, int temp, int m) 
 struct LdsSeq16 {
     uint16_t *lane0;  // &row[base][lane] as 16-bit
     int hs;
+    // entries 2i, 2i + 1 as one dword: a read that may alias the 16-bit stores
+    // of set() (a plain uint32_t read may be moved above them: strict aliasing)
+    __device__ __forceinline__ uint32_t pair(int i) const {
+        typedef uint32_t __attribute__((may_alias)) u32a;
+        return *(const u32a *)(lane0 + i * hs);
+    }
     __device__ __forceinline__ int get(int p) const { return lane0[(p >> 1) * hs + (p & 1)]; }
     __device__ __forceinline__ void set(int p, int e) const { lane0[(p >> 1) * hs + (p & 1)] = (uint16_t)e; }
     __device__ __forceinline__ bool less(int a, int b) const { return (a >> 5) < (b >> 5); }  // keys only, as std::sort
@@ -1495,7 +1511,10 @@ struct R1Prep {
     uint32_t ordp0, ordp1, symp, hw;
 };
 
-template <bool LT = false, class Path>
+// GEN = false (the FastSCL-LUT kernels without R1L): every R1 node has its ranks in
+// the op record (MF_R1_RK, one quanta row) -- the host takes the R1L instantiation
+// otherwise -- so the rank-table and std::sort paths are not compiled.
+template <bool LT = false, bool GEN = true, class Path>
 __device__ __forceinline__ R1Prep r1_prep(const FastPlan &P, const Mem &M, const MOp &op, Path st, int gbase, int L,
                                           int lane, int temp, uint32_t *lds_wave, uint32_t T2 = 0u,
                                           const uint8_t *tb = nullptr) {
@@ -1505,10 +1524,10 @@ __device__ __forceinline__ R1Prep r1_prep(const FastPlan &P, const Mem &M, const
     const uint16_t *rk = P.r1_rank + op.tab;
     const double *vq = P.vcl + (size_t)op.vrow * v;
     // MF_VUNI: one quanta row and one rank row for all elements, in registers
-    const bool uni = op.flags & MF_VUNI, rku = op.flags & MF_R1_RK;
+    const bool uni = !GEN || (op.flags & MF_VUNI), rku = !GEN || (op.flags & MF_R1_RK);
     const int s16 = lane & 15;
-    const uint32_t rrow = uni && !rku && s16 < v ? (uint32_t)rk[s16] : 0u;
-    const double vrow = uni && s16 < v ? vq[s16] : 0.0;
+    const uint32_t rrow = GEN && uni && !rku && s16 < v ? (uint32_t)rk[s16] : 0u;
+    (void)vq;
     // rank << 1 | sign of element j's symbol: from the op record's words (MF_R1_RK), the node's
     // one rank row in a register (MF_VUNI), or the per-element rank table
     const uint64_t RK = ((uint64_t)(uint32_t)op.tab2 << 32) | (uint32_t)op.r_row;
@@ -1585,7 +1604,7 @@ __device__ __forceinline__ R1Prep r1_prep(const FastPlan &P, const Mem &M, const
             u16x2 ep[16];
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const uint32_t d = 2 * i < temp ? *(const uint32_t *)(seq.lane0 + i * seq.hs) : 0u;  // entries 2i, 2i + 1
+                const uint32_t d = 2 * i < temp ? seq.pair(i) : 0u;  // entries 2i, 2i + 1
                 const uint32_t e0 = d & 0xffffu, e1 = d >> 16;
                 const uint32_t lo = 2 * i < end ? ((e0 >> 5) << 10) | ((uint32_t)(2 * i) << 5) | (e0 & 31u) : 0xffffu;
                 const uint32_t hi = 2 * i + 1 < end ? ((e1 >> 5) << 10) | ((uint32_t)(2 * i + 1) << 5) | (e1 & 31u) : 0xffffu;
@@ -1612,7 +1631,7 @@ __device__ __forceinline__ R1Prep r1_prep(const FastPlan &P, const Mem &M, const
                     }
                 }
             }
-        } else {
+        } else if constexpr (GEN) {
             stl::sort_small_prefix(seq, 0, temp, m);  // only ord[0, m) is read
 #pragma unroll
             for (int q = 0; q < kMaxM; ++q)
@@ -1652,14 +1671,14 @@ __device__ __forceinline__ void r1_small(const FastPlan &P, const Mem &M, const 
 // R1 nodes of <= 32 elements with L = 8 for all the wave's frame sets: the
 // argsorts set by set, then the layers of the sets interleaved (their fork
 // chains overlap), each set stopping at its first identity layer (r1_layers).
-template <bool LT, int NS, class Path>
+template <bool LT, bool GEN, int NS, class Path>
 __device__ __forceinline__ void r1_multi(const FastPlan &P, const Mem (&Mv)[NS], const MOp &op, Path (&st)[NS], int *sel_all,
                                          int sstride, int gl, int gbase, int lane, uint32_t *lds_wave, uint32_t T2,
                                          uint8_t *tb) {
     const int temp = op.cnt, v = P.v;
     const int m = kMaxM < temp ? kMaxM : temp;  // L = 8
     const double *vq = P.vcl + (size_t)op.vrow * v;
-    const bool uni = op.flags & MF_VUNI;
+    const bool uni = !GEN || (op.flags & MF_VUNI);
     const double vrow = uni && (lane & 15) < v ? vq[lane & 15] : 0.0;
     if constexpr (LT)
         if (op.flags & MF_SFG) stage_tab(tb, T2, (op.flags & MF_SGG) ? lane : (lane & 31));
@@ -1668,7 +1687,7 @@ __device__ __forceinline__ void r1_multi(const FastPlan &P, const Mem (&Mv)[NS],
     for (int s = 0; s < NS; ++s) {  // set s in slot 0 (rotate_sets)
         if ((QPD_EXP_FSCL & 64) && temp > 16) pr[0] = R1Prep{0x1a418820u, 6u, 0u, 0u};  // (ord 0..6)
         else
-        pr[0] = r1_prep<LT>(P, Mv[0].set(s), op, st[0], gbase, 8, lane, temp, lds_wave, T2, tb);
+        pr[0] = r1_prep<LT, GEN>(P, Mv[0].set(s), op, st[0], gbase, 8, lane, temp, lds_wave, T2, tb);
         rotate_sets(st);
         rotate_sets(pr);
     }
@@ -1692,7 +1711,7 @@ __device__ __forceinline__ void r1_multi(const FastPlan &P, const Mem (&Mv)[NS],
             const int o = gbase + origin[s];
             own[s] = (int)(layer < 6 ? __builtin_amdgcn_ubfe(pr[s].ordp0, 5 * layer, 5) : pr[s].ordp1);
             const uint32_t sym = __builtin_amdgcn_ubfe(pr[s].symp, 4 * layer, 4);
-            const double own_ms = fabs(uni ? shfld(vrow, (int)sym) : vq[(size_t)own[s] * v + sym]);
+            const double own_ms = fabs(!GEN || uni ? shfld(vrow, (int)sym) : vq[(size_t)own[s] * v + sym]);
             kf[s] = st[s].pm + shfld(own_ms, o);
             done[s] = keep_all8(__builtin_bit_cast(uint64_t, st[s].pm), __builtin_bit_cast(uint64_t, kf[s]), gl);
             all = all && done[s];
@@ -2014,6 +2033,12 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
 #ifndef QPD_WPE2_FSCL
 #define QPD_WPE2_FSCL 4
 #endif
+#ifndef QPD_COLD_SPEC
+#define QPD_COLD_SPEC 0
+#endif
+#ifndef QPD_R1_GEN
+#define QPD_R1_GEN 0
+#endif
 #ifndef QPD_BX_PIPE
 #define QPD_BX_PIPE 0  // BOTX slot operands loaded one slot ahead
 #endif
@@ -2049,6 +2074,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
     constexpr bool kList = (KIND == K_SCL_LUT || KIND == K_FASTSCL_LUT);
     // staged BOT3 loads: the list kinds (SCL-LUT, FastSCL-LUT)
     constexpr bool kLazy = QPD_BOT3_LAZY && kList;
+    constexpr bool kFast = (KIND == K_FASTSC_LUT || KIND == K_FASTSCL_LUT) && !(QPD_EXP_FSCL & 256);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
     // rows of all sets interleaved, each set's selection scratch as its next two
     // rows: set s's slots at sel_all + s * 64, its junk slots NS * 64 words on
@@ -2147,12 +2173,78 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                 if (!kLazy || op.type != OP_BOT3) pre = fetch_pre(P, nxt, lane, vlane);
             }
             const int fl = op.flags;
+            // special nodes, FastSCLUT.cpp:46-107 / FastSCLLUTDecoder.cpp:82-213
+            auto run_special = [&]() {
+              if constexpr (kFast) {
+                  // the sets one after the other, one copy of the code: set s runs in
+                  // stv[0] (the sets' states rotate; back in place after NS steps) --
+                  // the special nodes' code is not in the instruction cache twice
+                  if constexpr (KIND == K_FASTSCL_LUT && L8) {
+                    if ((op.type == OP_R0 || op.type == OP_REP) && !(QPD_EXP_FSCL & 512)) {
+                        r0rep_multi<kLdsTab>(P, Mv, op, stv, sel_all, sstride, gl, gbase, lane, cur.T2, tb);
+                        return;
+                    }
+                    if (op.type == OP_R1 && (op.cnt <= stl::kThreshold || (fl & MF_R1_LDS)) && !(QPD_EXP_FSCL & 1024)) {
+                        r1_multi<kLdsTab, R1L || QPD_R1_GEN>(P, Mv, op, stv, sel_all, sstride, gl, gbase, lane, lds_dyn, cur.T2, tb);
+                        return;
+                    }
+                    // without R1L every R1 node of > 16 elements has its LDS tail (the host
+                    // takes the R1L instantiation otherwise) and FastSCL-LUT has no SPC ops
+                    // (H7): nothing is left for the generic special_op
+#ifndef QPD_KEEP_SPECOP
+                    if constexpr (!R1L) return;
+#endif
+                  }
+#if QPD_SPEC_ROT
+#pragma unroll 1
+                  for (int s = 0; s < NS; ++s) {
+                    special_op<kList, L8, R1L>(P, Mv[0].set(s), op, stv[0], sel_all + sstride * s, NS * sstride, gl, gbase,
+                                               L, lane, lds_dyn);
+                    rotate_sets(stv);
+                  }
+#else
+#pragma unroll
+                  for (int s = 0; s < NS; ++s)
+                    special_op<kList, L8, R1L>(P, Mv[s], op, stv[s], sel_all + sstride * s, NS * sstride, gl, gbase, L, lane,
+                                               lds_dyn);
+#endif
+              }
+            };
+            // (QPD_COLD_SPEC: the special-node ops as a branch the compiler is told is
+            // rare, ahead of the switch -- its spill code then goes there, not into BOT3)
+            if constexpr (kFast && (QPD_COLD_SPEC & 1)) {
+                if (__builtin_expect(op.type >= OP_R0 && op.type <= OP_SPC, 0)) {
+                    run_special();
+                    goto op_done;
+                }
+            }
             switch (op.type) {
                 case OP_BOT3:
                     if constexpr (KIND == K_FASTSCL_LUT && L8 && !QPD_EXP_NO_BOTX) {
-                        if (fl & MF_BOTX) {
-                            if (kLazy && oi + 1 < P.nops) pre = fetch_pre(P, nxt, lane, vlane);
+                        if (fl & MF_BOTX)
+#if QPD_COLD_SPEC & 2
+                            [[unlikely]]
+#endif
+                        {
+#ifndef QPD_BX_LATEPRE
+#define QPD_BX_LATEPRE 0
+#endif
+                            if (kLazy && oi + 1 < P.nops && !QPD_BX_LATEPRE) pre = fetch_pre(P, nxt, lane, vlane);
+#ifndef QPD_BX_ROT
+#define QPD_BX_ROT 0  // A/B: the sets one after the other through a one-set botx_op
+#endif
+                            if constexpr (QPD_BX_ROT && NS > 1) {
+#pragma unroll 1
+                                for (int s = 0; s < NS; ++s) {  // set s in slot 0 (rotate_sets)
+                                    const Mem m1[1] = {Mv[0].set(s)};
+                                    const int32_t *const y1[1] = {yv[s]};
+                                    botx_op<kLdsTab>(P, m1, op, y1, *reinterpret_cast<PathT<PW1>(*)[1]>(&stv[0]), cur.T, cur.T2,
+                                                     gl, gbase, L, sel_all + sstride * s, NS * sstride, lane, tb);
+                                    rotate_sets(stv);
+                                }
+                            } else
                             botx_op<kLdsTab>(P, Mv, op, yv, stv, cur.T, cur.T2, gl, gbase, L, sel_all, sstride, lane, tb);
+                            if (kLazy && oi + 1 < P.nops && QPD_BX_LATEPRE) pre = fetch_pre(P, nxt, lane, vlane);
                             break;
                         }
                     }
@@ -2336,36 +2428,11 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                         }
                     }
                     break;
-                default: if constexpr (KIND == K_FASTSC_LUT || KIND == K_FASTSCL_LUT) {  // special nodes, FastSCLUT.cpp:46-107 / FastSCLLUTDecoder.cpp:82-213
-                  // the sets one after the other, one copy of the code: set s runs in
-                  // stv[0] (the sets' states rotate; back in place after NS steps) --
-                  // the special nodes' code is not in the instruction cache twice
-                  if constexpr (KIND == K_FASTSCL_LUT && L8) {
-                    if (op.type == OP_R0 || op.type == OP_REP) {
-                        r0rep_multi<kLdsTab>(P, Mv, op, stv, sel_all, sstride, gl, gbase, lane, cur.T2, tb);
-                        break;
-                    }
-                    if (op.type == OP_R1 && (op.cnt <= stl::kThreshold || (fl & MF_R1_LDS))) {
-                        r1_multi<kLdsTab>(P, Mv, op, stv, sel_all, sstride, gl, gbase, lane, lds_dyn, cur.T2, tb);
-                        break;
-                    }
-                  }
-#if QPD_SPEC_ROT
-#pragma unroll 1
-                  for (int s = 0; s < NS; ++s) {
-                    special_op<kList, L8, R1L>(P, Mv[0].set(s), op, stv[0], sel_all + sstride * s, NS * sstride, gl, gbase,
-                                               L, lane, lds_dyn);
-                    rotate_sets(stv);
-                  }
-#else
-#pragma unroll
-                  for (int s = 0; s < NS; ++s)
-                    special_op<kList, L8, R1L>(P, Mv[s], op, stv[s], sel_all + sstride * s, NS * sstride, gl, gbase, L, lane,
-                                               lds_dyn);
-#endif
-                  break;
-                }
+                default:
+                    if constexpr (kFast && !(QPD_COLD_SPEC & 1)) run_special();
+                    break;
             }
+        op_done:
 #ifdef QPD_STAMPS
             __builtin_amdgcn_s_waitcnt(0);
             {
