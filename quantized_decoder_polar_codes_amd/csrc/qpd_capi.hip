@@ -1318,7 +1318,8 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
         if (c->kind == QPD_FASTSCL_LUT && m.type == qpd::OP_R1 &&
             ((m.cnt > qpd::stl::kThreshold && !(m.flags & qpd::MF_R1_LDS)) || (QPD_R1L_RK && d->l8 && !(m.flags & qpd::MF_R1_RK))))
             d->r1l = true;
-    const bool pw1_ok = c->kind == QPD_SCL_LUT ? NS <= 2 : (c->kind == QPD_FASTSCL_LUT && NS == 2 && d->l8 && !d->r1l);
+    // (SCL-LUT only with the root pre-pass: those kernels have no channel reads, lut_fast_kernel kChan)
+    const bool pw1_ok = c->kind == QPD_SCL_LUT ? NS <= 2 && Ly.pre : (c->kind == QPD_FASTSCL_LUT && NS == 2 && d->l8 && !d->r1l);
     if (pw1_ok && !getenv("QPD_NO_PW1")) d->pw1 = compact_pointer_fields({&mops, &pp.st1, &pp.st2});
     d->pfx_nops = (int)pp.st1.size();
     d->pfx2_nops = (int)pp.st2.size();

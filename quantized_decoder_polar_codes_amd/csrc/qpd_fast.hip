@@ -907,7 +907,7 @@ __device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], u
 #define QPD_BOT3_LAZY 1
 #endif
 // LT: the folded parent's lookups (MF_BFG) from its table staged as bytes at tb (lut_lds).
-template <bool kList, bool L8, bool LAZY, bool LT, int NS, class PF, class Path>
+template <bool kList, bool L8, bool LAZY, bool LT, bool CH, int NS, class PF, class Path>
 __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], const MOp &op,
                                         const int32_t *const (&y)[NS], Path (&st)[NS], uint32_t Tf0, uint32_t T2, int gl,
                                         int gbase, int L, int *sel, int sstride, int lane, PF &&prefetch_next,
@@ -954,7 +954,7 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
         }
     } else {
 #pragma unroll
-        for (int s = 0; s < NS; ++s) x[s][0] = sym_word<true>(P, M[s], op, y[s], gbase + pfield(st[s].ps, op.sh_src), 0);  // W3
+        for (int s = 0; s < NS; ++s) x[s][0] = sym_word<CH>(P, M[s], op, y[s], gbase + pfield(st[s].ps, op.sh_src), 0);  // W3
     }
     // ---- q0 left: W2 = f(W3); q1: W1 = f(W2)
 #pragma unroll
@@ -1237,7 +1237,7 @@ __device__ __forceinline__ BxSlot bx_load(const FastPlan &P, const MOp &op, int 
     return s;
 }
 
-template <bool LT, int NS, class Path>
+template <bool LT, bool CH, int NS, class Path>
 __device__ __forceinline__ void botx_op(const FastPlan &P, const Mem (&M)[NS], const MOp &op, const int32_t *const (&y)[NS],
                                         Path (&st)[NS], uint32_t Tf0, uint32_t T2, int gl, int gbase, int L, int *sel,
                                         int sstride, int lane, uint8_t *tb) {
@@ -1260,7 +1260,7 @@ __device__ __forceinline__ void botx_op(const FastPlan &P, const Mem (&M)[NS], c
         }
     } else {
 #pragma unroll
-        for (int s = 0; s < NS; ++s) x[s][0] = sym_word<true>(P, M[s], op, y[s], gbase + pfield(st[s].ps, op.sh_src), 0);
+        for (int s = 0; s < NS; ++s) x[s][0] = sym_word<CH>(P, M[s], op, y[s], gbase + pfield(st[s].ps, op.sh_src), 0);
     }
     (void)Tf0;
 #pragma unroll 1  // (unrolled: 18 % slower)
@@ -2075,6 +2075,10 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
     // staged BOT3 loads: the list kinds (SCL-LUT, FastSCL-LUT)
     constexpr bool kLazy = QPD_BOT3_LAZY && kList;
     constexpr bool kFast = (KIND == K_FASTSC_LUT || KIND == K_FASTSCL_LUT) && !(QPD_EXP_FSCL & 256);
+    // channel reads inside the decode (MF_CHAN: codes without the root pre-pass); the
+    // one-pointer-word SCL-LUT instantiations run only op lists with the pre-pass
+    // (build_fast; +1.1 % SCL-LUT, -1.3 % when FastSCL-LUT's dropped them too, r05z5)
+    constexpr bool kChan = !(PW1 && KIND == K_SCL_LUT);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
     // rows of all sets interleaved, each set's selection scratch as its next two
     // rows: set s's slots at sel_all + s * 64, its junk slots NS * 64 words on
@@ -2238,17 +2242,17 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                                 for (int s = 0; s < NS; ++s) {  // set s in slot 0 (rotate_sets)
                                     const Mem m1[1] = {Mv[0].set(s)};
                                     const int32_t *const y1[1] = {yv[s]};
-                                    botx_op<kLdsTab>(P, m1, op, y1, *reinterpret_cast<PathT<PW1>(*)[1]>(&stv[0]), cur.T, cur.T2,
+                                    botx_op<kLdsTab, kChan>(P, m1, op, y1, *reinterpret_cast<PathT<PW1>(*)[1]>(&stv[0]), cur.T, cur.T2,
                                                      gl, gbase, L, sel_all + sstride * s, NS * sstride, lane, tb);
                                     rotate_sets(stv);
                                 }
                             } else
-                            botx_op<kLdsTab>(P, Mv, op, yv, stv, cur.T, cur.T2, gl, gbase, L, sel_all, sstride, lane, tb);
+                            botx_op<kLdsTab, kChan>(P, Mv, op, yv, stv, cur.T, cur.T2, gl, gbase, L, sel_all, sstride, lane, tb);
                             if (kLazy && oi + 1 < P.nops && QPD_BX_LATEPRE) pre = fetch_pre(P, nxt, lane, vlane);
                             break;
                         }
                     }
-                    bot3_op<kList, L8, kLazy, kLdsTab>(P, Mv, op, yv, stv, cur.T, cur.T2, gl, gbase, L, sel_all, sstride, lane, [&]() {
+                    bot3_op<kList, L8, kLazy, kLdsTab, kChan>(P, Mv, op, yv, stv, cur.T, cur.T2, gl, gbase, L, sel_all, sstride, lane, [&]() {
                         if (oi + 1 < P.nops) pre = fetch_pre(P, nxt, lane, vlane);
                     }, tb);
                     break;
@@ -2300,7 +2304,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                             else QPD_FG(true, 1, 1);
                         }
 #undef QPD_FG
-                    } else if (fl & MF_CHAN) {
+                    } else if (kChan && (fl & MF_CHAN)) {
                         if (op.type == OP_F) fg_chan_op<false>(P, Mv, op, yv, usrc, cur.T, lane);
                         else fg_chan_op<true>(P, Mv, op, yv, usrc, cur.T, lane);
                     } else if (op.type == OP_F)
@@ -2323,7 +2327,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                         dm[s] = 0;
                         none[s][0] = 0;
                         if (kList || !frozen) {
-                            const uint32_t W = sym_word<true>(P, Mv[s], op, yv[s], gbase + pfield(stv[s].ps, op.sh_src), 0, 2);
+                            const uint32_t W = sym_word<kChan>(P, Mv[s], op, yv[s], gbase + pfield(stv[s].ps, op.sh_src), 0, 2);
                             uint32_t idx = ((W & 15u) << 4) | ((W >> 4) & 15u);
                             if (right)
                                 idx |= (Mv[s].ld(fl & MF_U_LDS, op.u_row, gbase + pfield(stv[s].U(), op.sh_u)) & 1u) << 8;
