@@ -1309,14 +1309,14 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     place_syncs(mops, c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT);
     // one pointer word: the list kinds at one or two frame sets (the instantiations
     // fast_kernel() has); FastSCL-LUT only at two sets with L = 8 and no r1_large
-#ifndef QPD_R1L_RK
-#define QPD_R1L_RK 1
-#endif
-    // R1 nodes the lean argsort of the R1L = false kernels cannot take: > 16 elements
-    // without their LDS tail (r1_large), or (L = 8) without ranks in the op record
+    // Special nodes the lean code of the R1L = false kernels cannot take: R1 nodes of > 16
+    // elements without their LDS tail (r1_large), or (L = 8) R1 nodes without ranks in the
+    // op record and R0 / REP nodes without one quanta row
     for (const qpd::MOp &m : mops)
-        if (c->kind == QPD_FASTSCL_LUT && m.type == qpd::OP_R1 &&
-            ((m.cnt > qpd::stl::kThreshold && !(m.flags & qpd::MF_R1_LDS)) || (QPD_R1L_RK && d->l8 && !(m.flags & qpd::MF_R1_RK))))
+        if (c->kind == QPD_FASTSCL_LUT &&
+            ((m.type == qpd::OP_R1 &&
+              ((m.cnt > qpd::stl::kThreshold && !(m.flags & qpd::MF_R1_LDS)) || (d->l8 && !(m.flags & qpd::MF_R1_RK)))) ||
+             (d->l8 && (m.type == qpd::OP_R0 || m.type == qpd::OP_REP) && !(m.flags & qpd::MF_VUNI))))
             d->r1l = true;
     // (SCL-LUT only with the root pre-pass: those kernels have no channel reads, lut_fast_kernel kChan)
     const bool pw1_ok = c->kind == QPD_SCL_LUT ? NS <= 2 && Ly.pre : (c->kind == QPD_FASTSCL_LUT && NS == 2 && d->l8 && !d->r1l);

@@ -1742,13 +1742,18 @@ __device__ __forceinline__ void r1_multi(const FastPlan &P, const Mem (&Mv)[NS],
 // R0 / REP nodes with L = 8 for all the wave's frame sets, interleaved element
 // by element (their sums are dependent fp64 chains in the reference's order,
 // H5; the sets' chains overlap).
-template <bool LT, int NS, class Path>
+// GEN = false (the FastSCL-LUT kernels without R1L): every R0 / REP node has one quanta
+// row (MF_VUNI; the host takes the R1L instantiation otherwise).  With the byte-table
+// slot (LT) the two sums' terms of each symbol, (l < 0)|l| and (l >= 0)|l|, are staged
+// in it once per node and each element reads both with one ds_read_b128 (the same
+// doubles as the selects on the quanta: the sums are unchanged).
+template <bool LT, bool GEN, int NS, class Path>
 __device__ __forceinline__ void r0rep_multi(const FastPlan &P, const Mem (&Mv)[NS], const MOp &op, Path (&st)[NS], int *sel_all,
                                             int sstride, int gl, int gbase, int lane, uint32_t T2, uint8_t *tb) {
     const int fl = op.flags, temp = op.cnt, v = P.v;
     const bool rep = op.type == OP_REP, sl = fl & MF_SRC_LDS, dl = fl & MF_DST_LDS;
     const double *vq = P.vcl + (size_t)op.vrow * v;  // row d-1, position temp*node
-    const bool uni = fl & MF_VUNI;
+    const bool uni = !GEN || (fl & MF_VUNI);
     const double vr = uni && (lane & 15) < v ? vq[lane & 15] : 0.0;
     int src[NS];
     double kk[NS], kf[NS];
@@ -1760,6 +1765,12 @@ __device__ __forceinline__ void r0rep_multi(const FastPlan &P, const Mem (&Mv)[N
     const int n8 = (temp + 7) >> 3;
     if constexpr (LT)
         if (fl & MF_SFG) stage_tab(tb, T2, (fl & MF_SGG) ? lane : (lane & 31));
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    d2 *const qt = (d2 *)(tb + 512);  // (LT, !GEN) the symbols' terms, after the f / g tables' 512 B
+    if constexpr (LT && !GEN) {
+        if (lane < 16) qt[lane] = d2{vr < 0 ? fabs(vr) : 0.0, vr >= 0 ? fabs(vr) : 0.0};
+        lds_order();
+    }
 #pragma unroll 1
     for (int w = 0; w < n8; ++w) {
         uint32_t word[NS];
@@ -1771,12 +1782,19 @@ __device__ __forceinline__ void r0rep_multi(const FastPlan &P, const Mem (&Mv)[N
 #pragma unroll
             for (int s = 0; s < NS; ++s) {
                 const uint32_t sym = (word[s] >> (4 * i)) & 15u;
+                if constexpr (LT && !GEN) {
+                    const d2 t = qt[sym];
+                    kk[s] += t.x;
+                    if (rep) kf[s] += t.y;
+                    continue;
+                }
                 const double l = uni ? shfld(vr, (int)sym) : vq[(size_t)(8 * w + i) * v + sym];
                 kk[s] += l < 0 ? fabs(l) : 0.0;  // :88-95 / :176-180, (l<0)·|l|, (l>=0)·|l| as selects
                 if (rep) kf[s] += l >= 0 ? fabs(l) : 0.0;
             }
         }
     }
+    if constexpr (LT && !GEN) lds_order();  // (the slot's next writer comes after these reads)
     const int nwo = (temp + 31) >> 5;
     const uint32_t m = temp < 32 ? ((1u << temp) - 1u) : 0xffffffffu;
 #pragma unroll
@@ -2036,9 +2054,6 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
 #ifndef QPD_COLD_SPEC
 #define QPD_COLD_SPEC 0
 #endif
-#ifndef QPD_R1_GEN
-#define QPD_R1_GEN 0
-#endif
 #ifndef QPD_BX_PIPE
 #define QPD_BX_PIPE 0  // BOTX slot operands loaded one slot ahead
 #endif
@@ -2185,19 +2200,17 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                   // the special nodes' code is not in the instruction cache twice
                   if constexpr (KIND == K_FASTSCL_LUT && L8) {
                     if ((op.type == OP_R0 || op.type == OP_REP) && !(QPD_EXP_FSCL & 512)) {
-                        r0rep_multi<kLdsTab>(P, Mv, op, stv, sel_all, sstride, gl, gbase, lane, cur.T2, tb);
+                        r0rep_multi<kLdsTab, R1L>(P, Mv, op, stv, sel_all, sstride, gl, gbase, lane, cur.T2, tb);
                         return;
                     }
                     if (op.type == OP_R1 && (op.cnt <= stl::kThreshold || (fl & MF_R1_LDS)) && !(QPD_EXP_FSCL & 1024)) {
-                        r1_multi<kLdsTab, R1L || QPD_R1_GEN>(P, Mv, op, stv, sel_all, sstride, gl, gbase, lane, lds_dyn, cur.T2, tb);
+                        r1_multi<kLdsTab, R1L>(P, Mv, op, stv, sel_all, sstride, gl, gbase, lane, lds_dyn, cur.T2, tb);
                         return;
                     }
                     // without R1L every R1 node of > 16 elements has its LDS tail (the host
                     // takes the R1L instantiation otherwise) and FastSCL-LUT has no SPC ops
                     // (H7): nothing is left for the generic special_op
-#ifndef QPD_KEEP_SPECOP
                     if constexpr (!R1L) return;
-#endif
                   }
 #if QPD_SPEC_ROT
 #pragma unroll 1
