@@ -2051,9 +2051,6 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
 #ifndef QPD_WPE2_FSCL
 #define QPD_WPE2_FSCL 4
 #endif
-#ifndef QPD_COLD_SPEC
-#define QPD_COLD_SPEC 0
-#endif
 #ifndef QPD_BX_PIPE
 #define QPD_BX_PIPE 0  // BOTX slot operands loaded one slot ahead
 #endif
@@ -2227,41 +2224,12 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
 #endif
               }
             };
-            // (QPD_COLD_SPEC: the special-node ops as a branch the compiler is told is
-            // rare, ahead of the switch -- its spill code then goes there, not into BOT3)
-            if constexpr (kFast && (QPD_COLD_SPEC & 1)) {
-                if (__builtin_expect(op.type >= OP_R0 && op.type <= OP_SPC, 0)) {
-                    run_special();
-                    goto op_done;
-                }
-            }
             switch (op.type) {
                 case OP_BOT3:
                     if constexpr (KIND == K_FASTSCL_LUT && L8 && !QPD_EXP_NO_BOTX) {
-                        if (fl & MF_BOTX)
-#if QPD_COLD_SPEC & 2
-                            [[unlikely]]
-#endif
-                        {
-#ifndef QPD_BX_LATEPRE
-#define QPD_BX_LATEPRE 0
-#endif
-                            if (kLazy && oi + 1 < P.nops && !QPD_BX_LATEPRE) pre = fetch_pre(P, nxt, lane, vlane);
-#ifndef QPD_BX_ROT
-#define QPD_BX_ROT 0  // A/B: the sets one after the other through a one-set botx_op
-#endif
-                            if constexpr (QPD_BX_ROT && NS > 1) {
-#pragma unroll 1
-                                for (int s = 0; s < NS; ++s) {  // set s in slot 0 (rotate_sets)
-                                    const Mem m1[1] = {Mv[0].set(s)};
-                                    const int32_t *const y1[1] = {yv[s]};
-                                    botx_op<kLdsTab, kChan>(P, m1, op, y1, *reinterpret_cast<PathT<PW1>(*)[1]>(&stv[0]), cur.T, cur.T2,
-                                                     gl, gbase, L, sel_all + sstride * s, NS * sstride, lane, tb);
-                                    rotate_sets(stv);
-                                }
-                            } else
+                        if (fl & MF_BOTX) {
+                            if (kLazy && oi + 1 < P.nops) pre = fetch_pre(P, nxt, lane, vlane);
                             botx_op<kLdsTab, kChan>(P, Mv, op, yv, stv, cur.T, cur.T2, gl, gbase, L, sel_all, sstride, lane, tb);
-                            if (kLazy && oi + 1 < P.nops && QPD_BX_LATEPRE) pre = fetch_pre(P, nxt, lane, vlane);
                             break;
                         }
                     }
@@ -2446,10 +2414,9 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                     }
                     break;
                 default:
-                    if constexpr (kFast && !(QPD_COLD_SPEC & 1)) run_special();
+                    if constexpr (kFast) run_special();
                     break;
             }
-        op_done:
 #ifdef QPD_STAMPS
             __builtin_amdgcn_s_waitcnt(0);
             {
