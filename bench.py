@@ -244,7 +244,7 @@ def run_rank(args, ctx, wl):
                  f"(128 -> 16 levels); decoder tables: {args.luts}"
                  + (f" designed at {args.design_snr:g} dB by lutgen.py" if args.luts == "mindistortion" else "")
                  + "; resident in HBM"),
-        "config": {"workload": f"{args.kind} N={args.N} K={args.K} L={args.L} Q=16 (5G-NR PW code, no CRC)",
+        "config": {"workload": f"{args.kind} N={args.N} K={args.K}{(' L=' + str(args.L)) if 'SCL' in args.kind else ''} Q=16 (5G-NR PW code, no CRC)",
                    "decoder": args.kind, "N": args.N, "K": args.K, "L": args.L, "v": 16,
                    "frames_per_gpu_per_step": frames, "ebn0_db": args.ebn0, "luts": args.luts,
                    "parallelism": f"dp{ctx.world} (frames sharded by global frame id, RCCL counter all-reduce)"},
@@ -419,7 +419,7 @@ def mc_rank(args, ctx, wl):
             "ber": r.ber, "bler": r.bler, "bit_errors": r.bit_errors, "block_errors": r.block_errors,
             "stopped_early": r.stopped_early, "dtype": "u8", "data": "synthetic (qpd_mc_frames, Philox keyed by "
             "global frame id: identical frames and counters at any rank count)",
-            "config": {"workload": f"{args.kind} N={args.N} K={args.K} L={args.L} Q=16 Monte-Carlo point",
+            "config": {"workload": f"{args.kind} N={args.N} K={args.K}{(' L=' + str(args.L)) if 'SCL' in args.kind else ''} Q=16 Monte-Carlo point",
                        "ebn0_db": args.ebn0, "mc_frames": F, "stop_rule": f"Nblkerrs > {stop}" if stop else "none "
                        "(MaxBlock branch)", "batch_per_rank": args.frames, "luts": args.luts,
                        "parallelism": f"dp{ctx.world} (frames sharded by global frame id, RCCL counter all-reduce)"}}
