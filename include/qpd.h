@@ -302,6 +302,12 @@ typedef struct qpd_info {
                                  reference's traversal of this code (N log2 N for the
                                  SC/SCL kinds; fewer where special nodes skip subtrees):
                                  the algorithmic unit of the roofline (bench.py) */
+    int32_t fast_variant;     /* fast engine: which decode kernel instantiation the plan
+                                 runs -- bit 0: one pointer word per path (PW1); bit 1:
+                                 the general special-node instantiation (R1L: R1 nodes
+                                 beyond the LDS tail or without op-record ranks, R0 / REP
+                                 nodes without one quanta row); 0 otherwise */
+    int32_t reserved0;
 } qpd_info;
 /* qpd_info.last_engine: no decode yet, the GPU kernels (qpd_decode*, the GPU
  * branch of the host-buffer calls, qpd_mc_decode), or the host engine. */

@@ -122,6 +122,8 @@ class QpdInfo(ctypes.Structure):
         ("prefix_ops", _i32),
         ("last_engine", _i32),
         ("lookups_per_path", _i64),
+        ("fast_variant", _i32),
+        ("reserved0", _i32),
     ]
 
 

@@ -1704,6 +1704,8 @@ int qpd_get_info(const qpd_decoder *d, qpd_info *info) {
         if (o.type == qpd::OP_F || o.type == qpd::OP_G) lk += d->N >> (o.d + 1);
         else if (o.type == qpd::OP_LEAF_L || o.type == qpd::OP_LEAF_R) lk += 1;
     info->lookups_per_path = lk;
+    info->fast_variant = d->engine == QPD_ENGINE_FAST ? (d->pw1 ? 1 : 0) | (d->r1l ? 2 : 0) : 0;
+    info->reserved0 = 0;
     return QPD_OK;
 }
 

@@ -172,3 +172,22 @@ def test_botx_ca(seed, qpd, oracle_mod, monkeypatch):
     want = oracle_mod.decode_lut_ca("CA-FastSCL-LUT", p, K, A, 8, fm, sym, node_type=nt)
     assert_frames_equal(a.decode_batch(sym), want, a, f"botx-ca-{seed}")
     assert_frames_equal(b.decode_batch(sym), want, b, f"nobotx-ca-{seed}")
+
+
+def test_bench_codes_run_the_lean_kernels(qpd, oracle_mod):
+    """The bench workloads decode on the kernels the bench measures: one pointer
+    word per path, and for FastSCL-LUT the lean special-node instantiation (no R1L);
+    tables whose R0 / REP nodes read per-position quanta take the general one
+    (qpd_info.fast_variant), with the same bits as the oracle."""
+    import bench
+    from quantized_decoder_polar_codes_amd import lut as LU
+
+    for kind in ("SCL-LUT", "FastSCL-LUT"):
+        wl = bench.workload(1024, 512, 8, kind, 64, 2.0)
+        assert wl.dec.info()["fast_variant"] == 1, (kind, wl.dec.info()["fast_variant"])
+    p = LU.random_luts(1024, 16, seed=5, distinct_mags=3)  # quanta per position: no one-row nodes
+    dec = qpd.from_packed("FastSCL-LUT", p, 512, wl.fm, L=8, node_type=wl.nt, engine="fast")
+    assert dec.info()["fast_variant"] & 2
+    sym = np.random.default_rng(5).integers(0, 16, size=(64, 1024), dtype=np.int32)
+    want = oracle_mod.decode_lut("FastSCL-LUT", p, 512, 8, wl.fm, sym, node_type=wl.nt)
+    assert_frames_equal(dec.decode_batch(sym), want, dec, "fscl-general-variant")
