@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define QPD_ABI_VERSION 5
+#define QPD_ABI_VERSION 6
 
 /* Decoder kinds (the reference's class names). */
 enum qpd_kind {

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("QPD_LIB") or os.path.join(HERE, "libqpd.so")
  QPD_SCL_LLOYD) = range(15)
 FLOAT_KINDS = (QPD_SC_FLOAT, QPD_SCL_FLOAT, QPD_CASCL_FLOAT, QPD_FASTSC_FLOAT, QPD_FASTSCL_FLOAT, QPD_SC_UNIFORM,
                QPD_SCL_UNIFORM, QPD_SC_LLOYD, QPD_SCL_LLOYD)
-ABI_VERSION = 5
+ABI_VERSION = 6
 QPD_ENGINE_AUTO, QPD_ENGINE_GENERIC, QPD_ENGINE_FAST = range(3)
 QPD_OK, QPD_E_INVALID, QPD_E_UNSUPPORTED, QPD_E_DEVICE, QPD_E_INPUT = 0, -1, -2, -3, -4
 
