@@ -191,3 +191,24 @@ def test_bench_codes_run_the_lean_kernels(qpd, oracle_mod):
     sym = np.random.default_rng(5).integers(0, 16, size=(64, 1024), dtype=np.int32)
     want = oracle_mod.decode_lut("FastSCL-LUT", p, 512, 8, wl.fm, sym, node_type=wl.nt)
     assert_frames_equal(dec.decode_batch(sym), want, dec, "fscl-general-variant")
+
+
+@pytest.mark.parametrize("kind,env", [("FastSCL-LUT", "QPD_NO_R1RK"), ("SCL-LUT", "QPD_NO_PW1")])
+def test_lean_kernel_equals_general_at_scale(kind, env, qpd, monkeypatch):
+    """2^18 bench frames -- more than the oracle decodes in a test -- give the same
+    bits on the bench kernel (fast_variant 1) and on the general instantiation
+    (FastSCL-LUT without op-record ranks: R1L; SCL-LUT with two pointer words), a
+    size-independent check of the lean kernel at the bench's scale."""
+    import bench
+
+    wl = bench.workload(1024, 512, 8, kind, 1 << 18, 2.0)
+    assert wl.dec.info()["fast_variant"] == 1
+    monkeypatch.setenv(env, "1")
+    gen = qpd.from_packed(kind, wl.packed, 512, wl.fm, L=8, node_type=wl.nt, engine="fast")
+    monkeypatch.delenv(env)
+    assert gen.info()["fast_variant"] != 1
+    a = wl.dec.decode_batch(wl.sym)
+    b = gen.decode_batch(wl.sym)
+    import torch
+
+    assert torch.equal(a, b) if hasattr(a, "cpu") else np.array_equal(a, b)
