@@ -14,7 +14,7 @@ from quantized_decoder_polar_codes_amd import _lib, codes as C, lut as LU  # noq
 
 kind = sys.argv[1] if len(sys.argv) > 1 else "SCL-LUT"
 N, K, L, F = (int(x) for x in sys.argv[2:6]) if len(sys.argv) > 5 else (1024, 512, 8, 262144)
-names = ["F", "G", "LEAF_L", "LEAF_R", "COMB", "R0", "R1", "REP", "SPC", "BOT3"]
+names = ["F", "G", "LEAF_L", "LEAF_R", "COMB", "R0", "R1", "REP", "SPC", "BOT3", "IMPORT", "EXPORT"]
 import bench  # noqa: E402
 
 _wl = bench.workload(N, K, L, kind, F, 2.0)  # the bench workload (MinDistortion, 2 dB)
