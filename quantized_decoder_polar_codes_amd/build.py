@@ -93,6 +93,8 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     os.replace(LIB + ".tmp", LIB)
+    with open(os.path.join(odir, "BUILD_ID"), "w") as f:  # tools/build_variant.sh links against these objects
+        f.write(bid + "\n")
     return LIB
 
 

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -20,8 +21,8 @@
 namespace qpd {
 const void *fast_kernel_single(int kind, int sets);              // qpd_k_fast.hip
 const void *prefix_kernel(int kind, int sets, bool pw1);         // qpd_k_fast.hip
-const void *fast_kernel_scl(int sets, bool l8);                  // qpd_k_scl.hip
-const void *fast_kernel_scl_pw1(int sets, bool l8);              // qpd_k_scl1.hip
+const void *fast_kernel_scl(int sets, bool l8, bool w16);        // qpd_k_scl.hip
+const void *fast_kernel_scl_pw1(int sets, bool l8, bool w16);    // qpd_k_scl1.hip
 const void *fast_kernel_fscl(int sets, bool l8, bool r1l);       // qpd_fast_fscl.hip
 const void *fast_kernel_fscl_pw1(int sets, bool l8, bool r1l);   // qpd_fast_fscl1.hip
 const void *generic_kernel(int fam, int dom, bool wide);         // qpd_k_generic.hip
@@ -87,6 +88,7 @@ struct qpd_decoder {
     DeviceBuf mc_pref, mc_crc;  // qpd_mc_frames: info bits before each word; CRC contribution per message bit
     int sets = 1;  // fast engine: frame sets per wave (lut_fast_kernel NS)
     bool l8 = false;  // fast engine: list decoder with L = 8 (select_survivors8)
+    bool w16 = false; // fast engine: SCL-LUT with 9 <= L <= 16 (lane groups of 16, select_survivors16)
     bool r1l = false;  // fast engine: an R1 node needs r1_large (the R1L instantiation)
     bool pw1 = false;  // fast engine: one pointer word per path (compact_pointer_fields)
     bool pre = false;         // fast engine pre-mode: root_pre_kernel, then the decode on its rows
@@ -374,7 +376,7 @@ bool bot3_mixed(int kind, const int32_t *node_type, const double *vcl, int N, in
             any = true;
         }
     }
-    // diagnosis: QPD_BOTX_SEL = allowed types (bit 1 R0, 2 R1, 3 REP) | size-4 (bit 4) / size-2 (bit 5)
+#ifdef QPD_DIAG  // diagnostic builds only: QPD_BOTX_SEL = allowed types (bit 1 R0, 2 R1, 3 REP) | size-4 (bit 4) / size-2 (bit 5)
     if (const char *e = getenv("QPD_BOTX_SEL")) {
         const int sel = atoi(e);
         for (int i = 0; i < 6; ++i) {
@@ -382,6 +384,7 @@ bool bot3_mixed(int kind, const int32_t *node_type, const double *vcl, int N, in
             if (x && (!(sel & (1 << x)) || !(sel & (i < 2 ? 16 : 32)))) return false;
         }
     }
+#endif
     *ty = t;
     return any;
 }
@@ -888,11 +891,13 @@ bool plan_prefix(const std::vector<qpd::MOp> &ops, const FastOwner &own, int L, 
     }
     pp.st1.assign(ops.begin(), ops.begin() + s1);
     pp.st1.insert(pp.st1.end(), exp1.begin(), exp1.end());
-    // stage 2 (L > 4): up to the op with the third information leaf
+    // stage 2 (4 < L <= 8): up to the op with the third information leaf.  Not above L = 8:
+    // mink's 2L > 16 candidates go through libstdc++'s introsort there, whose order of tied
+    // live metrics the stable L = 4 selection would not reproduce (H1).
     size_t s2 = s1;
     for (int inf = 0; s2 < ops.size() && inf + info_leaves(ops[s2]) <= 2; ++s2) inf += info_leaves(ops[s2]);
     std::vector<char> live2[2];
-    if (L <= 4 || getenv("QPD_NO_PFX2") || s2 <= s1 || s2 >= ops.size() || !live_in(ops, s2, own, live2)) {
+    if (L <= 4 || L > qpd::kMaxL || getenv("QPD_NO_PFX2") || s2 <= s1 || s2 >= ops.size() || !live_in(ops, s2, own, live2)) {
         pp.rest = imp1;
         pp.rest.insert(pp.rest.end(), ops.begin() + s1, ops.end());
         return true;
@@ -981,12 +986,12 @@ constexpr int kDefaultSets = QPD_DEFAULT_SETS;
 
 // The decode kernel instantiation of a plan (nullptr: none, the launch fails).
 // pw1: the op list's pointer fields fit one word (compact_pointer_fields).
-const void *fast_kernel(int kind, int sets, bool l8, bool r1l, bool pw1) {
+const void *fast_kernel(int kind, int sets, bool l8, bool r1l, bool pw1, bool w16) {
     switch (kind) {
         case QPD_SC_LUT:
         case QPD_FASTSC_LUT: return pw1 || r1l ? nullptr : qpd::fast_kernel_single(kind, sets);
-        case QPD_SCL_LUT: return r1l ? nullptr : pw1 ? qpd::fast_kernel_scl_pw1(sets, l8) : qpd::fast_kernel_scl(sets, l8);
-        case QPD_FASTSCL_LUT: return pw1 ? qpd::fast_kernel_fscl_pw1(sets, l8, r1l) : qpd::fast_kernel_fscl(sets, l8, r1l);
+        case QPD_SCL_LUT: return r1l ? nullptr : pw1 ? qpd::fast_kernel_scl_pw1(sets, l8, w16) : qpd::fast_kernel_scl(sets, l8, w16);
+        case QPD_FASTSCL_LUT: return w16 ? nullptr : pw1 ? qpd::fast_kernel_fscl_pw1(sets, l8, r1l) : qpd::fast_kernel_fscl(sets, l8, r1l);
         default: return nullptr;
     }
 }
@@ -1097,9 +1102,15 @@ int init_task_queue(qpd_decoder *d) {
 
 #ifdef QPD_STAMPS
 // Diagnostic builds: the per-op-class cycle accumulators every decoder's
-// kernels add to (qpd_debug_stamps), one device buffer per process.
-unsigned long long *stamp_buffer() {
-    static unsigned long long *buf = nullptr;
+// kernels add to (qpd_debug_stamps), one device buffer per device (qpd_debug_stamps reads the
+// current device's).
+unsigned long long *stamp_buffer() {  // one per device (the current one)
+    static std::mutex mu;
+    static std::map<int, unsigned long long *> bufs;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    unsigned long long *&buf = bufs[dev];
     if (!buf && hipMalloc(&buf, 64 * sizeof(unsigned long long)) == hipSuccess)
         (void)hipMemset(buf, 0, 64 * sizeof(unsigned long long));
     return buf;
@@ -1134,13 +1145,6 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
         if (slot == 2) return dd >= 1 ? brows(dd) : 0;
         return brows(dd);
     };
-    auto lds_rows = [&](int D) {
-        int r = 0;
-        for (int dd = D; dd <= n; ++dd)
-            for (int sl = 0; sl < 3; ++sl)
-                if (use[sl][dd]) r += rows_of(sl, dd);
-        return r;
-    };
     auto assign = [&](FastLayout &L, int &rl, int &rg) {
         rl = rg = 0;
         for (int dd = 0; dd <= n; ++dd) {  // grouped by depth (see FastLayout)
@@ -1165,6 +1169,7 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     if (const char *e = getenv("QPD_SETS")) if (atoi(e) == 3 && c->kind == QPD_SCL_LUT && d->L == 8) d->sets = 3;
 #endif
     d->l8 = (c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT) && d->L == 8;
+    d->w16 = c->kind == QPD_SCL_LUT && d->L > qpd::kMaxL;
     const int NS = d->sets;
     FastLayout Ly;
     Ly.ns = NS;
@@ -1217,23 +1222,30 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     // shallow depths.
     int budget = NS == 1 ? 6 * 1024 : NS == 2 ? 10 * 1024 : 15 * 1024;
     if (const char *e = getenv("QPD_LDS_BUDGET")) budget = atoi(e);
-    while (Ly.D <= n && NS * (qpd::kSelInts * 4 + lds_rows(Ly.D) * 256) + d->lds_tab_bytes > budget) ++Ly.D;
-    F.lds_from = Ly.D;
-    int rl = 0, rg = 0;
-    assign(Ly, rl, rg);
     // FastSCL R1 nodes of 17..32 elements sort in the wave's LDS tail of the
-    // deeper levels (MF_R1_LDS): pad the rows so that the tail holds cnt / 2 rows
-    {
+    // deeper levels (MF_R1_LDS): rows of padding so that the tail holds cnt / 2
+    // rows -- part of the LDS the budget bounds
+    auto r1_pad = [&](const FastLayout &Lt) {
         int pad = 0;
         for (const qpd::Op &o : s.ops)
             if (c->kind == QPD_FASTSCL_LUT && o.type == qpd::OP_R1 && (N >> o.d) > qpd::stl::kThreshold &&
-                (N >> o.d) <= 32 && Ly.lds(o.d + 1)) {
-                const int have = NS * (Ly.lds_end - Ly.lds_base[o.d + 1]), need = (N >> o.d) / 2;
+                (N >> o.d) <= 32 && Lt.lds(o.d + 1)) {
+                const int have = NS * (Lt.lds_end - Lt.lds_base[o.d + 1]), need = (N >> o.d) / 2;
                 if (have < need) pad = std::max(pad, (need - have + NS - 1) / NS);
             }
-        rl += pad;
-        Ly.lds_end += pad;
+        return pad;
+    };
+    int rl = 0, rg = 0;
+    for (;; ++Ly.D) {
+        assign(Ly, rl, rg);
+        const int pad = r1_pad(Ly);
+        if (Ly.D > n || NS * (qpd::kSelInts * 4 + (rl + pad) * 256) + d->lds_tab_bytes <= budget) {
+            rl += pad;
+            Ly.lds_end += pad;
+            break;
+        }
     }
+    F.lds_from = Ly.D;
     F.R0_row = Ly.R[0];
     F.R0_lds = Ly.lds(0);
     F.H_row = F.K_row = F.I_row = rg;
@@ -1371,7 +1383,7 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         const hipError_t oe =
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fast_kernel(d->kind, d->sets, d->l8, d->r1l, d->pw1), 64,
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fast_kernel(d->kind, d->sets, d->l8, d->r1l, d->pw1, d->w16), 64,
                                                          d->lds_bytes);
         if (oe != hipSuccess || per_cu <= 0) per_cu = 16;
         mw = std::max(1, ncu) * per_cu;
@@ -1508,14 +1520,17 @@ int qpd_create(const qpd_config *cfg, qpd_decoder **out) {
     visit(s, c->kind, c->N, n, c->frozen_bits, (c->kind == QPD_FASTSC_LUT || c->kind == QPD_FASTSCL_LUT) ? c->node_type : nullptr, 0, 0);
     d->ops_host = s.ops;
     {
-        // L > 8 (2L > 16: libstdc++ introsort replayed per selection) runs on the generic engine
-        const bool fast_ok = dom == qpd::DOM_LUT && c->f_step == 0 && c->g_step == 0 && c->v <= 16 && d->L <= qpd::kMaxL;
+        // L > 8 (2L > 16: libstdc++ introsort, replayed where ties make it matter): SCL-LUT up to
+        // L = 16 on the fast engine (lane groups of 16, select_survivors16), the others on the generic one
+        const bool fast_ok = dom == qpd::DOM_LUT && c->f_step == 0 && c->g_step == 0 && c->v <= 16 &&
+                             (d->L <= qpd::kMaxL || (c->kind == QPD_SCL_LUT && d->L <= 2 * qpd::kMaxL));
         int want = c->engine;
         if (const char *e = getenv("QPD_ENGINE")) want = atoi(e);
         if (want == QPD_ENGINE_FAST && !fast_ok) {
             delete d;
             return fail(QPD_E_UNSUPPORTED,
-                        "fast engine needs LUT symbols with one table per node (f_step = g_step = 0), v <= 16 and L <= 8");
+                        "fast engine needs LUT symbols with one table per node (f_step = g_step = 0), v <= 16 and L <= 8 "
+                        "(SCL-LUT: L <= 16)");
         }
         d->engine = (want == QPD_ENGINE_GENERIC || !fast_ok) ? QPD_ENGINE_GENERIC : QPD_ENGINE_FAST;
     }
@@ -1721,7 +1736,7 @@ int fast_launch(qpd_decoder *d, qpd::FastPlan fp, const int32_t *in, int64_t Bc,
                 bool prefix = false) {
     const int sets = prefix ? d->pfx_sets : d->sets;
     const int64_t tw = (int64_t)fp.fpw * sets;  // frames per wave task
-    const void *kfn = prefix ? prefix_kernel(d->kind, sets, d->pw1) : fast_kernel(d->kind, d->sets, d->l8, d->r1l, d->pw1);
+    const void *kfn = prefix ? prefix_kernel(d->kind, sets, d->pw1) : fast_kernel(d->kind, d->sets, d->l8, d->r1l, d->pw1, d->w16);
     if (!kfn) return fail(QPD_E_INVALID, "bad kind");
     const int64_t fgroups = (Bc + tw - 1) / tw;
     int fgrid = (int)std::min<int64_t>(fgroups, d->max_waves);

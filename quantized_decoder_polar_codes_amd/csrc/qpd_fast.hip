@@ -778,10 +778,122 @@ __device__ __forceinline__ bool keep_all8(uint64_t K, uint64_t F, int gl) {
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// List sizes 9..16 (LM = 16: lane groups of 16 = one DPP row, 4 frames per
+// set).  mink (SCLLUTDecoder.cpp:8-21) sorts 2L > 16 candidates, so libstdc++
+// runs its introsort, which is NOT stable: with tied keys the survivors' order
+// is whatever the partitions leave (H1).  Without ties every correct sort
+// gives the same first L outputs, so the kernel ranks by counting and replays
+// the introsort only for a group whose first L ranks hold a tie:
+//  * strict identity (keep_all16): keeps strictly increasing, every flip
+//    strictly above the largest keep -- the unique sorted order puts keep j in
+//    slot j whatever the algorithm;
+//  * select_survivors16: stable ranks (key, reference index) against the 15
+//    row partners by DPP row rotations, plus a tie flag; groups with a tie
+//    among their first L ranks replay stl::sort_small_prefix (the generic
+//    engine's replay, stl_sort.hpp) on their first lane over the set's
+//    selection scratch, one group after the other.
+// Candidates are encoded keep j -> j, flip j -> 16 + j (flips after keeps, as
+// the reference's indices j < L <= L + j); lanes gl >= L are padding (+inf
+// keys, never scattered below L).
+// ---------------------------------------------------------------------------
+template <int R>
+__device__ __forceinline__ uint32_t dpp_ror(uint32_t x) {  // rotate within a row of 16 lanes
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x120 + R, 0xF, 0xF, false);
+}
+template <int R>
+__device__ __forceinline__ uint64_t dpp_ror64(uint64_t x) {
+    return ((uint64_t)dpp_ror<R>((uint32_t)(x >> 32)) << 32) | dpp_ror<R>((uint32_t)x);
+}
+
+__device__ __forceinline__ bool keep_all16(uint64_t K, uint64_t F, int gl, int gbase, int L) {
+    const uint64_t Kn = dpp64<kDppRowShl1>(K);  // keep of slot gl + 1
+    const uint64_t kl = shfl64(K, gbase + L - 1);
+    const bool ok = (gl >= L - 1 || K < Kn) && (gl >= L || F > kl);
+    return __builtin_amdgcn_ballot_w64(!ok) == 0;
+}
+
+// Stable ranks (key, index) against the row partners R..15 lanes away (as
+// rank8_partner), and whether any partner's key equals this lane's keep / flip.
+template <int R>
+__device__ __forceinline__ void rank16_all(uint64_t K, uint64_t F, int gl, int &rk, int &rf, bool &eqk, bool &eqf) {
+    if constexpr (R < 16) {
+        const uint64_t ok = dpp_ror64<R>(K), of = dpp_ror64<R>(F);
+        const uint64_t t = (uint64_t)((int)dpp_ror<R>((uint32_t)gl) < gl);  // partner index below
+        rk += ok < K + t;
+        rk += of < K;
+        rf += ok <= F;
+        rf += of < F + t;
+        eqk = eqk || ok == K || of == K;
+        eqf = eqf || ok == F || of == F;
+        rank16_all<R + 1>(K, F, gl, rk, rf, eqk, eqf);
+    }
+}
+
+// Index array of the serial replay in LDS (stl_sort.hpp Seq): keys by reference index.
+struct SelReplay16 {
+    int *idx;
+    const double *key;
+    __device__ int get(int p) { return idx[p]; }
+    __device__ void set(int p, int e) { idx[p] = e; }
+    __device__ bool less(int a, int b) { return key[a] < key[b]; }
+};
+
+__device__ __forceinline__ Sel select_survivors16(double kk, double kf, int gl, int gbase, int L, int lane, int *sel,
+                                                  int sj) {
+    const uint64_t kInfBits = 0x7ff0000000000000ull;
+    const bool pad = gl >= L;
+    const uint64_t K = pad ? kInfBits : __builtin_bit_cast(uint64_t, kk);
+    const uint64_t F = pad ? kInfBits : __builtin_bit_cast(uint64_t, kf);
+    int rk = F < K, rf = K <= F;
+    bool eqk = K == F, eqf = K == F;
+    rank16_all<1>(K, F, gl, rk, rf, eqk, eqf);
+    // a tie among the first L ranks changes the introsort's output (H1)
+    const bool tie = (rk < L && eqk) || (rf < L && eqf);
+    sel[rk < L && !pad ? gbase + rk : sj + lane] = gl;
+    sel[rf < L && !pad ? gbase + rf : sj + lane] = gl + 16;
+    lds_order();
+    int c = pad ? gl : sel[gbase + gl];
+    lds_order();
+    uint64_t slow = __builtin_amdgcn_ballot_w64(tie);
+    if (slow) {
+        // groups with a tie, one after the other: keys by reference index at sel
+        // (2L <= 32 doubles), the index array at the junk slots (2L ints)
+        double *key = (double *)sel;
+        int *idx = sel + sj;
+#pragma unroll 1
+        for (int g = 0; g < 64; g += 16) {
+            if (!((slow >> g) & 0xFFFFull)) continue;
+            if (gbase == g && !pad) {
+                key[gl] = kk;
+                key[L + gl] = kf;
+            }
+            lds_order();
+            if (lane == g) {
+                SelReplay16 seq{idx, key};
+                for (int p = 0; p < 2 * L; ++p) idx[p] = p;
+                stl::sort_small_prefix(seq, 0, 2 * L, L);  // libstdc++'s steps, first L outputs
+            }
+            lds_order();
+            if (gbase == g && !pad) {
+                const int e = idx[gl];
+                c = e < L ? e : e - L + 16;
+            }
+            lds_order();
+        }
+    }
+    Sel s;
+    s.upper = c >= 16;
+    s.parent = c & 15;
+    return s;
+}
+
 // Info leaf with quanta dm: keep the L best of {keep, flip} candidates.
 // Returns the new decision; `extra` words follow the surviving lineage.
 // `moved` (wave-uniform): the selection was not the identity (paths moved).
-template <bool L8, int NX, class Path>
+// LM: the list mode -- 8 (L = 8, groups of 8: DPP ranks), 16 (L = 9..16,
+// groups of 16), 0 (L <= 8, the generic stable ranks).
+template <int LM, int NX, class Path>
 __device__ __forceinline__ uint32_t leaf_fork(Path &st, double dm, int gl, int gbase, int L, int lane, int *sel, int sj,
                                               uint32_t (&extra)[NX], bool &moved) {
     const double kf = st.pm + fabs(dm);
@@ -789,10 +901,14 @@ __device__ __forceinline__ uint32_t leaf_fork(Path &st, double dm, int gl, int g
     // Fast path (about 2/3 of the info leaves on the bench channel): the
     // selection is the identity, the decision the hard one.
     moved = false;
-    if constexpr (L8)
+    if constexpr (LM == 8)
         if (keep_all8(__builtin_bit_cast(uint64_t, st.pm), __builtin_bit_cast(uint64_t, kf), gl)) return hd;
+    if constexpr (LM == 16)
+        if (keep_all16(__builtin_bit_cast(uint64_t, st.pm), __builtin_bit_cast(uint64_t, kf), gl, gbase, L)) return hd;
     moved = true;
-    const Sel sl = L8 ? select_survivors8(st.pm, kf, gl, gbase, lane, sel, sj) : select_survivors(st.pm, kf, gl, gbase, L, sel);
+    const Sel sl = LM == 8    ? select_survivors8(st.pm, kf, gl, gbase, lane, sel, sj)
+                   : LM == 16 ? select_survivors16(st.pm, kf, gl, gbase, L, lane, sel, sj)
+                              : select_survivors(st.pm, kf, gl, gbase, L, sel);
     const int p = gbase + sl.parent;
     const uint32_t dec = (uint32_t)lane_read((int)hd, p) ^ (sl.upper ? 1u : 0u);
     st.pm = pick(sl.upper, shfld(kf, p), shfld(st.pm, p));
@@ -803,7 +919,7 @@ __device__ __forceinline__ uint32_t leaf_fork(Path &st, double dm, int gl, int g
 }
 
 // One leaf decision for every set.  `frozen` is wave-uniform.
-template <bool kList, bool L8, int NS, int NX, class Path>
+template <bool kList, int LM, int NS, int NX, class Path>
 __device__ __forceinline__ void leaf_decide(Path (&st)[NS], const double (&dm)[NS], bool frozen, int gl, int gbase,
                                             int L, int lane, int *sel, int sstride, uint32_t (&extra)[NS][NX],
                                             uint32_t (&dec)[NS], bool (&moved)[NS]) {
@@ -826,7 +942,7 @@ __device__ __forceinline__ void leaf_decide(Path (&st)[NS], const double (&dm)[N
     }
 #pragma unroll
     for (int s = 0; s < NS; ++s)
-        dec[s] = leaf_fork<L8>(st[s], dm[s], gl, gbase, L, lane, sel + sstride * s, NS * sstride, extra[s], moved[s]);
+        dec[s] = leaf_fork<LM>(st[s], dm[s], gl, gbase, L, lane, sel + sstride * s, NS * sstride, extra[s], moved[s]);
 }
 
 // ---------------------------------------------------------------------------
@@ -845,7 +961,7 @@ __device__ __forceinline__ uint32_t g_pair(uint32_t T, uint32_t c2, uint32_t w2)
     return lut_vec<2>(T, w2, w2 >> 8, c2);
 }
 
-template <bool kList, bool L8, bool SPEC, int NS, class Path>
+template <bool kList, int LM, bool SPEC, int NS, class Path>
 __device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], uint32_t Tf, int fo, uint32_t Tg,
                                          double V, int vo, int fr, int gl, int gbase, int L, int lane, int *sel, int sstride,
                                          uint32_t (&c)[NS]) {
@@ -865,7 +981,7 @@ __device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], u
     // chain of the ~2/3 of forks that move nothing; a fork that moves paths
     // looks it up again from the surviving lineage's word.
     double sdm[NS];
-    if constexpr (kList && L8 && SPEC) {
+    if constexpr (kList && LM == 8 && SPEC) {
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             const uint32_t a = (x[s][1] >> 16) & 15u, b = (x[s][1] >> 20) & 15u;
@@ -874,13 +990,13 @@ __device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], u
         }
     }
 #endif
-    leaf_decide<kList, L8>(st, dm, fr & 1, gl, gbase, L, lane, sel, sstride, x, bl, moved);
+    leaf_decide<kList, LM>(st, dm, fr & 1, gl, gbase, L, lane, sel, sstride, x, bl, moved);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         x[s][1] = (x[s][1] & ~(1u << 24)) | (bl[s] << 24);
         const uint32_t a = (x[s][1] >> 16) & 15u, b = (x[s][1] >> 20) & 15u;
 #if QPD_SPEC_RIGHT
-        if constexpr (kList && L8 && SPEC) {
+        if constexpr (kList && LM == 8 && SPEC) {
             dm[s] = sdm[s];
             if (moved[s]) dm[s] = shfld(V, vo + 16 + (int)lut4(Tg, (bl[s] << 8) | (a << 4) | b));
             continue;
@@ -888,7 +1004,7 @@ __device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], u
 #endif
         if (kList || !(fr & 2)) dm[s] = shfld(V, vo + 16 + (int)lut4(Tg, (bl[s] << 8) | (a << 4) | b));
     }
-    leaf_decide<kList, L8>(st, dm, fr & 2, gl, gbase, L, lane, sel, sstride, x, br, moved);
+    leaf_decide<kList, LM>(st, dm, fr & 2, gl, gbase, L, lane, sel, sstride, x, br, moved);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const uint32_t bl2 = (x[s][1] >> 24) & 1u;
@@ -907,7 +1023,7 @@ __device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], u
 #define QPD_BOT3_LAZY 1
 #endif
 // LT: the folded parent's lookups (MF_BFG) from its table staged as bytes at tb (lut_lds).
-template <bool kList, bool L8, bool LAZY, bool LT, bool CH, int NS, class PF, class Path>
+template <bool kList, int LM, bool LAZY, bool LT, bool CH, int NS, class PF, class Path>
 __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], const MOp &op,
                                         const int32_t *const (&y)[NS], Path (&st)[NS], uint32_t Tf0, uint32_t T2, int gl,
                                         int gbase, int L, int *sel, int sstride, int lane, PF &&prefetch_next,
@@ -962,7 +1078,7 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
         const uint32_t w2 = lut_vec<4>(Tf0, x[s][0], x[s][0] >> 16, 0u);
         x[s][1] = w2 | (f_pair(Tf12, 0u, w2) << 16);
     }
-    bot_pair<kList, L8, LAZY>(st, x, Tf34, 0, Tg3, Vlo, 0, fr, gl, gbase, L, lane, sel, sstride, c);  // leaves 0, 1
+    bot_pair<kList, LM, LAZY>(st, x, Tf34, 0, Tg3, Vlo, 0, fr, gl, gbase, L, lane, sel, sstride, c);  // leaves 0, 1
     if constexpr (LAZY) {  // stage C's operands
         Tg0 = tab_ld(gt, p0 * 64, lane);
         Tf56 = tab_ld(ft, (p3 + 2) * 32, lane);
@@ -974,7 +1090,7 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
         x[s][1] = (x[s][1] & ~(3u << 25)) | (c[s] << 25);
         x[s][1] = (x[s][1] & ~(0xffu << 16)) | (g_pair(Tg1, c[s], x[s][1] & 0xffffu) << 16);
     }
-    bot_pair<kList, L8, LAZY>(st, x, Tf34, 256, Tg4, Vlo, 32, fr >> 2, gl, gbase, L, lane, sel, sstride, c);  // leaves 2, 3
+    bot_pair<kList, LM, LAZY>(st, x, Tf34, 256, Tg4, Vlo, 32, fr >> 2, gl, gbase, L, lane, sel, sstride, c);  // leaves 2, 3
     if constexpr (LAZY) {  // stage D's operands
         Tg2 = tab_ld(gt, (p1 + 1) * 64, lane);
         Tg6 = tab_ld(gt, (p3 + 3) * 64, lane);
@@ -987,14 +1103,14 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
         const uint32_t w2 = lut_vec<4>(Tg0, x[s][0], x[s][0] >> 16, c3);
         x[s][1] = w2 | (f_pair(Tf12, 3u, w2) << 16) | (c3 << 27);
     }
-    bot_pair<kList, L8, LAZY>(st, x, Tf56, 0, Tg5, Vhi, 0, fr >> 4, gl, gbase, L, lane, sel, sstride, c);  // leaves 4, 5
+    bot_pair<kList, LM, LAZY>(st, x, Tf56, 0, Tg5, Vhi, 0, fr >> 4, gl, gbase, L, lane, sel, sstride, c);  // leaves 4, 5
     if constexpr (LAZY) prefetch_next();
 #pragma unroll
     for (int s = 0; s < NS; ++s) {  // q2: W1 = g(W2, c2)
         x[s][1] = (x[s][1] & ~(3u << 25)) | (c[s] << 25);
         x[s][1] = (x[s][1] & ~(0xffu << 16)) | (g_pair(Tg2, c[s], x[s][1] & 0xffffu) << 16);
     }
-    bot_pair<kList, L8, LAZY>(st, x, Tf56, 256, Tg6, Vhi, 32, fr >> 6, gl, gbase, L, lane, sel, sstride, c);  // leaves 6, 7
+    bot_pair<kList, LM, LAZY>(st, x, Tf56, 256, Tg6, Vhi, 32, fr >> 6, gl, gbase, L, lane, sel, sstride, c);  // leaves 6, 7
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const uint32_t c2 = (x[s][1] >> 25) & 3u;
@@ -1302,7 +1418,7 @@ __device__ __forceinline__ void botx_op(const FastPlan &P, const Mem (&M)[NS], c
         if (QPD_BXE & 4) continue;
 #endif
         if (t2 == BX_PLAIN) {
-            bot_pair<true, true, false>(st, x, cur.tf, 0, cur.tg, cur.V, 0, fr >> (2 * k), gl, gbase, L, lane, sel, sstride, c);
+            bot_pair<true, 8, false>(st, x, cur.tf, 0, cur.tg, cur.V, 0, fr >> (2 * k), gl, gbase, L, lane, sel, sstride, c);
         } else {
             bx_spec_multi(st, x, t2, 2, 16, cur.V, gl, gbase, lane, sel, sstride, c);
         }
@@ -2063,7 +2179,11 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
 #ifndef QPD_WPE3
 #define QPD_WPE3 3
 #endif
-// NS frame sets per wave (see above); L8: list decoders with L = 8.
+#ifndef QPD_WPE_W16
+#define QPD_WPE_W16 4  // SCL-LUT at 9 <= L <= 16 (W16)
+#endif
+// NS frame sets per wave (see above); L8: list decoders with L = 8; W16: SCL-LUT with
+// 9 <= L <= 16 (lane groups of 16, select_survivors16).
 // LDS: NS * (lds_rows + 2) rows, set-interleaved (see Mem): a set's rows
 // 0..lds_rows-1 (grouped by depth, see FastLayout), then its selection scratch
 // as rows lds_rows (64 slots) and lds_rows + 1 (junk slots).
@@ -2077,13 +2197,16 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
 // prove the op records are never written and fetch them with scalar loads
 // instead of vector loads + readfirstlane, which drain vmcnt at every op.
 // PW1: one pointer word per path (PathT; the host packed the op list's fields).
-template <int KIND, int NS, bool L8, bool R1L = false, bool PFX = false, bool PW1 = false>
+template <int KIND, int NS, bool L8, bool R1L = false, bool PFX = false, bool PW1 = false, bool W16 = false>
 __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
+                                : W16 ? QPD_WPE_W16
                                 : NS == 2 ? (KIND == K_SCL_LUT && !PFX ? QPD_WPE2_SCL : KIND == K_FASTSCL_LUT ? QPD_WPE2_FSCL : QPD_WPE2)
                                 : KIND == K_FASTSCL_LUT ? QPD_WPE_FSCL : QPD_WPE1) void lut_fast_kernel(FastPlan P, const int32_t *__restrict__ in, int64_t B,
                                                                uint8_t *__restrict__ out,
                                                                const MOp *__restrict__ ops) {
     constexpr bool kList = (KIND == K_SCL_LUT || KIND == K_FASTSCL_LUT);
+    static_assert(!W16 || (KIND == K_SCL_LUT && !L8), "W16: SCL-LUT list sizes 9..16");
+    constexpr int LM = L8 ? 8 : W16 ? 16 : 0;  // list mode of the leaf forks (leaf_fork)
     // staged BOT3 loads: the list kinds (SCL-LUT, FastSCL-LUT)
     constexpr bool kLazy = QPD_BOT3_LAZY && kList;
     constexpr bool kFast = (KIND == K_FASTSC_LUT || KIND == K_FASTSCL_LUT) && !(QPD_EXP_FSCL & 256);
@@ -2233,7 +2356,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                             break;
                         }
                     }
-                    bot3_op<kList, L8, kLazy, kLdsTab, kChan>(P, Mv, op, yv, stv, cur.T, cur.T2, gl, gbase, L, sel_all, sstride, lane, [&]() {
+                    bot3_op<kList, LM, kLazy, kLdsTab, kChan>(P, Mv, op, yv, stv, cur.T, cur.T2, gl, gbase, L, sel_all, sstride, lane, [&]() {
                         if (oi + 1 < P.nops) pre = fetch_pre(P, nxt, lane, vlane);
                     }, tb);
                     break;
@@ -2315,7 +2438,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                             dm[s] = shfld(cur.V, (int)lut4(cur.T, idx));  // vcl[n-1][k][s] (H3)
                         }
                     }
-                    leaf_decide<kList, L8>(stv, dm, frozen, gl, gbase, L, lane, sel_all, sstride, none, dec, moved);
+                    leaf_decide<kList, LM>(stv, dm, frozen, gl, gbase, L, lane, sel_all, sstride, none, dec, moved);
 #pragma unroll
                     for (int s = 0; s < NS; ++s) {
                         Mv[s].st(fl & MF_DST_LDS, op.dst_row, lane, dec[s]);

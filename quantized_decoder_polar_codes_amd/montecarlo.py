@@ -168,8 +168,9 @@ def run_point(generate, decode, K: int, ebn0_db: float, batch: int, max_blocks: 
     Without a group, two ways to run the sharding of a ``world``-rank job in
     one process (tests of config C5's 8-rank split on one device):
     ``shard=(rank, world)`` (no early stop only) returns rank ``rank``'s
-    counters alone -- the ranks' results summed are the job's, which is what
-    the end-of-point all-reduce computes; ``virtual_world=W`` runs the W
+    counters alone, with ``blocks`` / ``frames_decoded`` its own frame count and
+    ``ber`` / ``bler`` over those frames -- the ranks' counters summed are the
+    job's, which is what the end-of-point all-reduce computes; ``virtual_world=W`` runs the W
     ranks' slices of every step in lock step, combining them as the per-step
     all-reduce / all-gather would (the stop rule's crossing may then fall in
     any rank's slice)."""
@@ -186,11 +187,13 @@ def run_point(generate, decode, K: int, ebn0_db: float, batch: int, max_blocks: 
     if stop_blkerrs is None:
         counted = (lambda lo, n, acc: gen_decode(lo, n, counts=acc)) if gen_decode is not None else None
         res = _run_point_all(step_fn, K, ebn0_db, batch, max_blocks, world, rank, group, count_device, counted)
-        if shard is not None:  # this rank's frames only
+        if shard is not None:  # this rank's frames only: its counters over its own frame count
             n = sum(max(0, min((rank + 1) * batch, min(world * batch, max_blocks - f0)) -
                        min(rank * batch, min(world * batch, max_blocks - f0)))
                     for f0 in range(0, max_blocks, world * batch))
-            res.frames_decoded = n
+            res.frames_decoded = res.blocks = n
+            res.ber = res.bit_errors / (K * n) if n else 0.0
+            res.bler = res.block_errors / n if n else 0.0
         return res
     if virtual_world > 1:
         assert group is None, "virtual_world: no group"

@@ -86,10 +86,12 @@ def test_special_folds_random_codes(N, seed, qpd, oracle_mod, monkeypatch):
 
 
 @pytest.mark.parametrize("N,K,mags", [(1024, 512, 2), (1024, 512, 3), (1024, 480, 2), (1024, 560, 4), (512, 300, 2)])
-def test_r1_bitplane_argsort(N, K, mags, qpd, oracle_mod):
-    """R1 nodes of 17..32 elements with one quanta row (MF_R1_RK): the argsort
-    replayed on bit planes in registers (r1_bitplane) on tie-heavy tables
-    (2-4 magnitudes: the partitions meet many equal keys) = the oracle."""
+def test_r1_masked_partition_argsort(N, K, mags, qpd, oracle_mod):
+    """R1 nodes of 17..32 elements with one quanta row (MF_R1_RK): the introsort's
+    partitions replayed in the LDS tail by partition_prefix_masked (>= / <= pivot
+    masks, only the swaps touch LDS), then the first m outputs as the m smallest
+    (rank, position) entries by packed 16-bit min trees (r1_prep), on tie-heavy
+    tables (2-4 magnitudes: the partitions meet many equal keys) = the oracle."""
     from quantized_decoder_polar_codes_amd import codes as C
     from quantized_decoder_polar_codes_amd import lut as LU
 
@@ -102,7 +104,7 @@ def test_r1_bitplane_argsort(N, K, mags, qpd, oracle_mod):
     sym = np.random.default_rng(K).integers(0, 16, size=(128, N), dtype=np.int32)
     want = oracle_mod.decode_lut("FastSCL-LUT", p, K, 8, fm, sym, node_type=nt)
     dec = qpd.from_packed("FastSCL-LUT", p, K, fm, L=8, node_type=nt, engine="fast")
-    assert_frames_equal(dec.decode_batch(sym), want, dec, f"r1-bitplane-{N}-{K}-{mags}")
+    assert_frames_equal(dec.decode_batch(sym), want, dec, f"r1-masked-{N}-{K}-{mags}")
 
 
 def test_special_folds_engage(qpd, monkeypatch):

@@ -42,6 +42,12 @@ def _node_type(N, K):
 ENGINES = ["auto", "generic"]  # auto = the fast kernel wherever the tables allow it
 
 
+def fast_engine_serves(kind, L):
+    """The fast engine takes L <= 8, and SCL-LUT (CA-SCL-LUT) up to L = 16 (lane groups of 16,
+    qpd_fast.hip select_survivors16); larger lists run on the generic engine."""
+    return L <= 8 or (L <= 16 and kind in ("SCL-LUT", "CA-SCL-LUT"))
+
+
 @pytest.mark.parametrize("engine", ENGINES)
 @pytest.mark.parametrize("path", golden_files(), ids=lambda p: os.path.basename(p)[:-4])
 def test_gpu_matches_golden(path, engine, qpd):
@@ -56,7 +62,7 @@ def test_gpu_matches_golden(path, engine, qpd):
         kw = {"A": int(g["A"])} if str(g["kind"]).startswith("CA-") else {}
         dec = qpd.from_packed(str(g["kind"]), golden_packed(g), K, g["frozen"], L=L, node_type=g["node_type"],
                               engine=engine, **kw)
-        assert dec.info()["engine"] == (2 if engine == "auto" and L <= 8 else 1)  # L > 8: generic engine
+        assert dec.info()["engine"] == (2 if engine == "auto" and fast_engine_serves(str(g["kind"]), L) else 1)
         got = dec.decode_batch(g["symbols"].astype(np.int32))
     assert_frames_equal(got, g["expected"], dec, f"golden-{os.path.basename(path)[:-4]}-{engine}")
 
@@ -111,7 +117,7 @@ def test_gpu_matches_oracle(N, K, L, tables, kind, engine, qpd, oracle_mod):
     want = oracle_mod.decode_lut(kind, p, K, L, fm, sym, node_type=nt)
     dec = qpd.from_packed(kind, p, K, fm, L=L, node_type=nt, engine=engine)
     if engine == "auto":
-        assert dec.info()["engine"] == (1 if tables == "perelem" or (L > 8 and kind in ("SCL-LUT", "FastSCL-LUT")) else 2)
+        assert dec.info()["engine"] == (2 if tables != "perelem" and fast_engine_serves(kind, L) else 1)
     got = dec.decode_batch(sym)
     redo = lambda rows: qpd.from_packed(kind, p, K, fm, L=L, node_type=nt, engine=engine).decode_batch(sym[rows])  # noqa: E731
     assert_frames_equal(got, want, dec, f"oracle-{kind}-{N}-{K}-{L}-{tables}-{engine}", redo, sym)
@@ -123,6 +129,8 @@ CA_CASES = [
     (64, 20, 24, 4, "minsum", 2.0),
     (128, 40, 24, 8, "minsum", 1.0),
     (128, 40, 24, 8, "random", 1.0),
+    (128, 40, 24, 16, "random", 1.0),  # L = 16: SCL on the fast engine's lane groups of 16
+    (256, 100, 24, 12, "minsum", 1.0),
     (256, 100, 11, 8, "minsum", 1.5),   # a shorter CRC (5G CRC11 taps)
     (512, 230, 24, 3, "minsum", 1.5),
     (1024, 488, 24, 8, "minsum", 1.5),

@@ -106,6 +106,10 @@ def test_shard_counters_sum_to_one_shot(world, batch, max_blocks):
     assert sum(p.bit_errors for p in parts) == want[2]
     assert sum(p.block_errors for p in parts) == want[3]
     assert sum(p.frames_decoded for p in parts) == max_blocks
+    for p in parts:  # each shard's rates are over its own frames
+        assert p.blocks == p.frames_decoded
+        assert p.bler == (p.block_errors / p.blocks if p.blocks else 0.0)
+        assert p.ber == (p.bit_errors / (K * p.blocks) if p.blocks else 0.0)
 
 
 @pytest.mark.parametrize("world,batch,max_blocks,stop", [(8, 16, 2000, 40), (8, 5, 600, 25), (3, 9, 600, 25),

@@ -14,7 +14,17 @@ UNITS=$(cd "$ROOT" && python3 -c "
 from quantized_decoder_polar_codes_amd import build
 for u, fl in build.UNITS: print(u + '|' + ' '.join(fl))")
 # VARIANT_UNITS="a.hip b.hip": compile only those, link the rest from the last
-# in-tree build (build/obj, build.py)
+# in-tree build (build/obj, build.py).  Refused when build/obj is not the current
+# tree's build (its BUILD_ID), and for flags that change a struct the host unit
+# fills (QPD_STAMPS adds FastPlan::stamps): then every unit must be rebuilt.
+if [ -n "${VARIANT_UNITS:-}" ]; then
+  case " $* " in *QPD_STAMPS*) echo "build_variant: VARIANT_UNITS with QPD_STAMPS changes FastPlan's layout; rebuild all units" >&2; exit 2;; esac
+  want=$(cd "$ROOT" && python3 -c "from quantized_decoder_polar_codes_amd import build; print(build.source_hash())")
+  have=$(cat "$ROOT/build/obj/BUILD_ID" 2>/dev/null || true)
+  if [ "$want" != "$have" ] || [ -n "${QPD_VARIANT_SRC:-}" ]; then
+    echo "build_variant: build/obj ($have) is not this tree's build ($want); run build.py or drop VARIANT_UNITS" >&2; exit 2
+  fi
+fi
 objs=()
 while IFS='|' read -r u fl; do
   o="$OUT/obj_$NAME/${u%.*}.o"

@@ -19,8 +19,24 @@ static void fork_hook(const double *key, int L) {
     int c = 2;
     if (sorted && below == 0) c = 0;
     else if (sorted && below == 1 && key[L + a] >= key[L - 2]) c = 1;
-    // detail: 10 * min(below, 8) + (sorted ? 0 : 100) + c
-    g_cases->push_back(c + 10 * (below < 9 ? below : 9) + (sorted ? 0 : 100));
+    // 2L > 16 (the W16 kernel, qpd_fast.hip select_survivors16): strict identity, and a tie
+    // among the first L stable ranks (the introsort replay)
+    bool strict = true;
+    for (int j = 0; j + 1 < L; ++j) strict = strict && key[j] < key[j + 1];
+    for (int j = 0; j < L; ++j) strict = strict && key[L + j] > key[L - 1];
+    bool tie = false;
+    for (int i = 0; i < 2 * L && !tie; ++i) {
+        int r = 0;
+        bool eq = false;
+        for (int k = 0; k < 2 * L; ++k) {
+            if (k == i) continue;
+            r += key[k] < key[i] || (key[k] == key[i] && k < i);
+            eq = eq || key[k] == key[i];
+        }
+        tie = r < L && eq;
+    }
+    // detail: 10 * min(below, 8) + (sorted ? 0 : 100) + c + (strict ? 1000 : 0) + (tie ? 2000 : 0)
+    g_cases->push_back(c + 10 * (below < 9 ? below : 9) + (sorted ? 0 : 100) + (strict ? 1000 : 0) + (tie ? 2000 : 0));
 }
 #define QPD_HOST_FORK_HOOK(k, L) fork_hook(k, L)
 #include "qpd_host.hpp"

@@ -19,7 +19,8 @@ so = "/tmp/fork_cases.so"
 subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-I", f"{ROOT}/include", "-I",
                 f"{ROOT}/quantized_decoder_polar_codes_amd/csrc", f"{ROOT}/tools/fork_cases.cpp", "-o", so], check=True)
 lib = ctypes.CDLL(so)
-N, K, L = 1024, 512, 8
+N, K = 1024, 512
+L = int(sys.argv[3]) if len(sys.argv) > 3 else 8
 F = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 ebn0 = float(sys.argv[2]) if len(sys.argv) > 2 else 2.0
 _, mb, fm, mm = C.construct_pw(N, K)
@@ -34,9 +35,12 @@ per = np.zeros(F, np.int64)
 n = lib.fc_run(ctypes.byref(dec._cfg), sym.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(F),
                cases.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(len(cases)), per.ctypes.data_as(ctypes.c_void_p))
 raw = cases[:n].reshape(F, -1)  # every frame forks at the same info leaves
+strict = (raw // 1000) % 2 == 1
+tie = raw >= 2000
 c = raw % 10
 below = (raw // 10) % 10
-unsorted = raw >= 100
+unsorted = (raw // 100) % 10 == 1
+print(f"  L={L}: strict identity {strict.mean():.3f}, tie among the first L ranks {tie.mean():.3f}")
 print("  flips below the largest keep (per fork):", {int(b): round(float(np.mean(below == b)), 3) for b in range(10)})
 print("  keeps not in stable order:", round(float(unsorted.mean()), 3))
 print(f"frames {F}, info-leaf forks per frame {c.shape[1]}")
