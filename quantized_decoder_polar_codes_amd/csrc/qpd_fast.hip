@@ -813,20 +813,21 @@ __device__ __forceinline__ bool keep_all16(uint64_t K, uint64_t F, int gl, int g
     return __builtin_amdgcn_ballot_w64(!ok) == 0;
 }
 
-// Stable ranks (key, index) against the row partners R..15 lanes away (as
-// rank8_partner), and whether any partner's key equals this lane's keep / flip.
+// Dense key ranks: how many of the group's candidates have a strictly smaller
+// key than this lane's keep / flip, counted against the 15 row partners (DPP
+// row rotations).  lt preserves the order of the keys among the 2L
+// candidates exactly (x < y <=> lt_x < lt_y), so the introsort replay below
+// compares 5-bit ranks instead of doubles.  Padding lanes carry +inf: never
+// smaller than anything.
 template <int R>
-__device__ __forceinline__ void rank16_all(uint64_t K, uint64_t F, int gl, int &rk, int &rf, bool &eqk, bool &eqf) {
+__device__ __forceinline__ void lt16_all(uint64_t K, uint64_t F, int &lk, int &lf) {
     if constexpr (R < 16) {
         const uint64_t ok = dpp_ror64<R>(K), of = dpp_ror64<R>(F);
-        const uint64_t t = (uint64_t)((int)dpp_ror<R>((uint32_t)gl) < gl);  // partner index below
-        rk += ok < K + t;
-        rk += of < K;
-        rf += ok <= F;
-        rf += of < F + t;
-        eqk = eqk || ok == K || of == K;
-        eqf = eqf || ok == F || of == F;
-        rank16_all<R + 1>(K, F, gl, rk, rf, eqk, eqf);
+        lk += ok < K;
+        lk += of < K;
+        lf += ok < F;
+        lf += of < F;
+        lt16_all<R + 1>(K, F, lk, lf);
     }
 }
 
@@ -839,25 +840,139 @@ struct SelReplay16 {
     __device__ bool less(int a, int b) { return key[a] < key[b]; }
 };
 
+// The group's array of 2L entries (lt << 5 | reference index), position p in
+// lane p (p < L) or lane p - L (p >= L, upper half-word): every lane holds
+// its keep's and its flip's starting positions.  w16_rd: the entry at a
+// group-uniform position (a ds_bpermute: the whole wave executes it);
+// w16_wr: this lane's word with that position's entry replaced.
+__device__ __forceinline__ uint32_t w16_rd(uint32_t E, int gbase, int L, int p) {
+    const bool hi = p >= L;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute((gbase + (hi ? p - L : p)) << 2, (int)E);
+    return hi ? w >> 16 : w & 0xFFFFu;
+}
+__device__ __forceinline__ uint32_t w16_wr(uint32_t E, int gl, int L, int p, uint32_t e) {
+    const bool hi = p >= L;
+    if (gl != (hi ? p - L : p)) return E;
+    return hi ? (E & 0xFFFFu) | (e << 16) : (E & 0xFFFF0000u) | e;
+}
+
+// The group's mask of positions (bit p) whose flag is set, from the lanes'
+// flags for their two positions (ballots; every lane gets its group's mask).
+__device__ __forceinline__ uint32_t w16_mask(bool c0, bool c1, int gbase, int L) {
+    const uint64_t b0 = __builtin_amdgcn_ballot_w64(c0), b1 = __builtin_amdgcn_ballot_w64(c1);
+    const uint32_t m = (1u << L) - 1u;
+    return ((uint32_t)(b0 >> gbase) & m) | (((uint32_t)(b1 >> gbase) & m) << L);
+}
+
+// Ranks of this lane's two packed u16 composites against the row partners' (R..15 lanes away).
+template <int R, class LessM, class V>
+__device__ __forceinline__ void rank16_packed(uint32_t X, LessM &lessm, V &acc) {
+    if constexpr (R < 16) {
+        const uint32_t Y = dpp_ror<R>(X);
+        acc += lessm(__builtin_bit_cast(V, Y));
+        acc += lessm(__builtin_bit_cast(V, __builtin_amdgcn_alignbit(Y, Y, 16)));
+        rank16_packed<R + 1>(X, lessm, acc);
+    }
+}
+
 __device__ __forceinline__ Sel select_survivors16(double kk, double kf, int gl, int gbase, int L, int lane, int *sel,
                                                   int sj) {
     const uint64_t kInfBits = 0x7ff0000000000000ull;
     const bool pad = gl >= L;
     const uint64_t K = pad ? kInfBits : __builtin_bit_cast(uint64_t, kk);
     const uint64_t F = pad ? kInfBits : __builtin_bit_cast(uint64_t, kf);
-    int rk = F < K, rf = K <= F;
-    bool eqk = K == F, eqf = K == F;
-    rank16_all<1>(K, F, gl, rk, rf, eqk, eqf);
-    // a tie among the first L ranks changes the introsort's output (H1)
-    const bool tie = (rk < L && eqk) || (rf < L && eqf);
-    sel[rk < L && !pad ? gbase + rk : sj + lane] = gl;
-    sel[rf < L && !pad ? gbase + rf : sj + lane] = gl + 16;
+    int lk = F < K, lf = K < F;
+    lt16_all<1>(K, F, lk, lf);
+    uint32_t E = pad ? 0xFFFFFFFFu : (((uint32_t)lk << 5) | (uint32_t)gl) | ((((uint32_t)lf << 5) | (uint32_t)(L + gl)) << 16);
+    // stl::partition_prefix(seq, 0, 2L, L) replayed by each group on its array
+    // (libstdc++ __introsort_loop's partitions, stl_sort.hpp): group-uniform f,
+    // l, depth limit and end in every lane of the group.
+    const int n2 = 2 * L;
+    int f = 0, l = n2, dl = 2 * stl::lg(n2), end = n2;
+    bool live = true, serial = false;
+#pragma unroll 1
+    while (__builtin_amdgcn_ballot_w64(live)) {
+        if (live && dl == 0) {  // heap-sort fallback: the group replays serially below
+            serial = true;
+            live = false;
+        }
+        --dl;
+        const int mid = f + (l - f) / 2;
+        // move_median_to_first(f, f + 1, mid, l - 1) on the ranks
+        const uint32_t ea = w16_rd(E, gbase, L, f + 1), eb = w16_rd(E, gbase, L, mid), ec = w16_rd(E, gbase, L, l - 1);
+        const uint32_t ef = w16_rd(E, gbase, L, f);
+        const uint32_t ra = ea >> 5, rb = eb >> 5, rc = ec >> 5;
+        int pick;
+        if (ra < rb) pick = rb < rc ? mid : ra < rc ? l - 1 : f + 1;
+        else pick = ra < rc ? f + 1 : rb < rc ? l - 1 : mid;
+        const uint32_t em = pick == mid ? eb : pick == f + 1 ? ea : ec;
+        if (live) {
+            E = w16_wr(E, gl, L, f, em);
+            E = w16_wr(E, gl, L, pick, ef);
+        }
+        // unguarded_partition(f + 1, l, pivot f): the left scan stops at ranks >= the
+        // pivot's, the right scan at ranks <= it.  A swap leaves the untouched
+        // positions as they were, so the k-th stops are the k-th such positions of
+        // the array before the partition (from the left / from the right) while they
+        // have not crossed; the scan that then runs on stops at the last right stop
+        // at the latest (its swapped-in entry): cut = min(next left stop, last right stop).
+        const uint32_t pv = em >> 5;
+        const uint32_t in = ((l < 32 ? (1u << l) : 0u) - 1u) & ~((2u << f) - 1u);  // positions [f + 1, l)
+        const uint32_t r0 = (E & 0xFFFFu) >> 5, r1 = E >> 21;
+        uint32_t GE = w16_mask(!pad && r0 >= pv, !pad && r1 >= pv, gbase, L) & in;
+        uint32_t LE = w16_mask(!pad && r0 <= pv, !pad && r1 <= pv, gbase, L) & in;
+        int a = GE ? __builtin_ctz(GE) : n2, b = LE ? 31 - __builtin_clz(LE) : -1, bprev = n2;
+        bool act = live && a < b;
+#pragma unroll 1
+        while (__builtin_amdgcn_ballot_w64(act)) {
+            const int pa = act ? a : 0, pb = act ? b : 0;
+            const uint32_t xa = w16_rd(E, gbase, L, pa), xb = w16_rd(E, gbase, L, pb);
+            if (act) {
+                E = w16_wr(E, gl, L, pa, xb);
+                E = w16_wr(E, gl, L, pb, xa);
+                GE &= GE - 1u;
+                LE &= ~(1u << pb);
+                bprev = pb;
+                a = GE ? __builtin_ctz(GE) : n2;
+                b = LE ? 31 - __builtin_clz(LE) : -1;
+                act = a < b;
+            }
+        }
+        if (live) {
+            const int cut = a < bprev ? a : bprev;
+            if (cut >= L && cut < end) end = cut;  // a block boundary past the first L positions
+            if (l - cut > stl::kThreshold) {
+                if (cut >= end) live = false;  // the reference's recursion on [cut, l) lies past the prefix
+                else f = cut;
+            } else {
+                l = cut;
+            }
+            live = live && l - f > stl::kThreshold;
+        }
+    }
+    // The final insertion sort of [0, end) is stable on the positions the partitions
+    // left: its first L outputs are the L smallest (rank, position) -- ranks of the
+    // composites (lt << 5 | position) counted against the row partners, packed u16.
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const uint32_t p0 = (uint32_t)gl, p1 = (uint32_t)(L + gl);
+    const uint32_t c0 = !pad && (int)p0 < end ? ((E & 0xFFE0u) | p0) : 0xFFFFu;
+    const uint32_t c1 = !pad && (int)p1 < end ? (((E >> 16) & 0xFFE0u) | p1) : 0xFFFFu;
+    const u16x2 X = __builtin_bit_cast(u16x2, c0 | (c1 << 16));
+    const u16x2 one = {1, 1};
+    auto lessm = [&](u16x2 y) { return __builtin_elementwise_min(__builtin_elementwise_sub_sat(X, y), one); };  // 1: y < x
+    u16x2 R = lessm(__builtin_bit_cast(u16x2, __builtin_amdgcn_alignbit(c0 | (c1 << 16), c0 | (c1 << 16), 16)));
+    rank16_packed<1>(c0 | (c1 << 16), lessm, R);
+    const int rk0 = R.x, rk1 = R.y;
+    const uint32_t cand0 = E & 31u, cand1 = (E >> 16) & 31u;
+    sel[rk0 < L && !pad ? gbase + rk0 : sj + lane] = (int)(cand0 < (uint32_t)L ? cand0 : cand0 - L + 16);
+    sel[rk1 < L && !pad ? gbase + rk1 : sj + lane] = (int)(cand1 < (uint32_t)L ? cand1 : cand1 - L + 16);
     lds_order();
     int c = pad ? gl : sel[gbase + gl];
     lds_order();
-    uint64_t slow = __builtin_amdgcn_ballot_w64(tie);
+    const uint64_t slow = __builtin_amdgcn_ballot_w64(serial);
     if (slow) {
-        // groups with a tie, one after the other: keys by reference index at sel
+        // groups that reached the depth limit (heap-sort fallback), one after the other:
+        // the whole replay on the group's first lane, keys by reference index at sel
         // (2L <= 32 doubles), the index array at the junk slots (2L ints)
         double *key = (double *)sel;
         int *idx = sel + sj;

@@ -335,6 +335,9 @@ class Engine {
             int dup = -1;  // an earlier path with the same inputs computed this node already
             for (int j = 0; j < i && dup < 0; ++j)
                 if ((d == 0 ? 0 : PS(j, d)) == src && (!ISG || PU(j, d + 1) == us) && PS(j, d + 1) == j) dup = j;
+#ifdef QPD_HOST_FG_HOOK
+            QPD_HOST_FG_HOOK(d, ISG, dup >= 0);  // diagnostic builds: how many path rows an f / g op shares
+#endif
             if (dup >= 0) {
                 PS(i, d + 1) = (uint8_t)dup;
                 continue;

@@ -45,6 +45,8 @@ ENGINES = ["auto", "generic"]  # auto = the fast kernel wherever the tables allo
 def fast_engine_serves(kind, L):
     """The fast engine takes L <= 8, and SCL-LUT (CA-SCL-LUT) up to L = 16 (lane groups of 16,
     qpd_fast.hip select_survivors16); larger lists run on the generic engine."""
+    if "SCL" not in kind:  # SC-LUT / FastSC-LUT: no list
+        return True
     return L <= 8 or (L <= 16 and kind in ("SCL-LUT", "CA-SCL-LUT"))
 
 

@@ -14,3 +14,17 @@ def test_stl_sort_matches_std_sort(tmp_path):
     r = subprocess.run([str(exe), "60000"], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches=0" in r.stdout
+
+
+def test_w16_parallel_replay_matches_std_sort(tmp_path):
+    """The W16 kernel's survivor selection for 2L > 16 candidates (qpd_fast.hip
+    select_survivors16: dense ranks, the introsort partitions replayed from
+    scan-stop masks, the final (rank, position) selection), emulated lane group
+    by lane group, gives std::sort's first L outputs (mink, H1) on tie-heavy
+    path-metric-like keys, dead (+inf) paths and all-equal lists, L = 9..16."""
+    exe = tmp_path / "w16_replay_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", os.path.join(ROOT, "tests", "native", "w16_replay_check.cpp"),
+                    "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe), "100000"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches=0" in r.stdout
