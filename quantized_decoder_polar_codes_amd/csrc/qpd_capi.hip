@@ -1376,6 +1376,15 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     rc = upload(d->g_tab, gt.data(), gt.size(), d->hs);
     if (rc) return rc;
     const int64_t per_wave = (int64_t)NS * F.glb_rows * 64 * 4;
+    {
+        // the byte tables' lookups address LDS offset 0 as the start of the dynamic
+        // allocation (qpd_fast.hip lut_lds): the kernel must declare no static LDS
+        hipFuncAttributes fa;
+        const void *kfn = fast_kernel(d->kind, d->sets, d->l8, d->r1l, d->pw1, d->w16);
+        if (!kfn) return fail(QPD_E_UNSUPPORTED, "fast plan: no decode kernel instantiation for this plan");
+        QPD_HIP(hipFuncGetAttributes(&fa, kfn));
+        if (fa.sharedSizeBytes != 0) return fail(QPD_E_DEVICE, "fast decode kernel declares static LDS");
+    }
     // Persistent grid: as many waves as can be resident at once.
     int mw = c->max_waves;
     if (mw <= 0) {

@@ -139,6 +139,11 @@ struct FastPlan {
 #define QPD_EXP_SLABMUL 1
 #endif
 
+#ifndef QPD_EXP_LUTMASK
+#define QPD_EXP_LUTMASK 0xFFFF  // timing experiments only (wrong results): 0x7F keeps every byte-table
+                                // lookup inside one 128-B LDS bank row (no bank conflicts)
+#endif
+
 #ifndef QPD_EXP_NO_BOTX
 #define QPD_EXP_NO_BOTX 0  // register-allocation experiments: botx_op compiled out (MF_BOTX ops then wrong)
 #endif
@@ -362,27 +367,83 @@ __device__ __forceinline__ void stage_tab(uint8_t *tb, uint32_t T, int dw) {
     *(uint2 *)(tb + 8 * dw) = b;
 }
 
-template <int NE, bool ISG>
-__device__ __forceinline__ uint32_t lut_lds(const uint8_t *tb, uint32_t A, uint32_t B, uint32_t hi) {
-    const uint32_t X = ((A << 4) & 0xF0F0F0F0u) | (B & 0x0F0F0F0Fu);
-    const uint32_t Y = (A & 0xF0F0F0F0u) | ((B >> 4) & 0x0F0F0F0Fu);
+// Bank swizzle of the g table's u = 1 half (QPD_GSWZ, a multiple of 8): entry
+// (1, i) sits at byte 256 + (i ^ QPD_GSWZ), so that the lookups of one path
+// pair that differ only in u -- the common case: a frame's paths share their
+// symbols and differ in their decisions -- fall on different LDS banks instead
+// of two dwords of one bank (ds_read_u8 banking: (byte / 4) mod 32 per 32-lane
+// half-wave).  Simulated on the bench workload (tools/bank_sim.py): the g
+// lookups' conflict cycles 44 % -> 17 % with 72; measured (profiles/r06f_*):
+// SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 15.8 % -> 10.0 % (SCL-LUT), 17.6 % ->
+// 11.1 % (FastSCL-LUT) -- but 3.3 % / 1.5 % slower: the swizzle's VALU (the
+// index bytes XOR u_byte * M: 6 per word of 8 lookups; 4 for M = 8, still -2.3 %)
+// costs more than the conflicts, VALU issue being the kernel's nearest ceiling
+// (a what-if without any conflicts and no extra VALU: +3.5 %).  Off; stage_tab
+// puts the u = 1 chunks at lane ^ QPD_GSWZ / 8 (gtab_dw).
+#ifndef QPD_GSWZ
+#define QPD_GSWZ 0
+#endif
+__device__ __forceinline__ int gtab_dw(int lane) { return lane ^ ((lane >> 5) * (QPD_GSWZ >> 3)); }
+
+// The staged tables sit at LDS offset TOFF of the wave's allocation (the kernel's
+// `tb`, offset 0: lut_fast_kernel puts them first; qpd_capi.hip checks that the
+// kernel declares no static LDS before them): the lookups address LDS through a
+// constant, which the compiler folds into each ds_read_u8's offset field.
+typedef __attribute__((address_space(3))) const uint8_t lds_u8;
+#ifndef QPD_LUT_PACK2
+#define QPD_LUT_PACK2 1  // lut_lds: the 8 results combined as 16-bit pairs (see there)
+#endif
+template <int NE, bool ISG, int TOFF = 0>
+__device__ __forceinline__ uint32_t lut_lds(uint32_t A, uint32_t B, uint32_t hi) {
+    lds_u8 *const tb = (lds_u8 *)(size_t)TOFF;
+    uint32_t X = ((A << 4) & 0xF0F0F0F0u) | (B & 0x0F0F0F0Fu);
+    uint32_t Y = (A & 0xF0F0F0F0u) | ((B >> 4) & 0x0F0F0F0Fu);
     uint32_t hx = 0, hy = 0;  // byte j = bit 2j / 2j+1 of hi (g: the u half)
     if constexpr (ISG) {
         hx = (((hi & 0x55u) * 0x02082080u) >> 7) & 0x01010101u;
         hy = ((((hi >> 1) & 0x55u) * 0x02082080u) >> 7) & 0x01010101u;
+        if constexpr (QPD_GSWZ != 0) {  // bytes of hx, hy are 0 / 1: X ^= hx * M by shifts (a
+            uint32_t sx = 0, sy = 0;      // 32-bit multiply is a quarter-rate VALU op)
+#pragma unroll
+            for (int bit = 3; bit < 8; ++bit)
+                if ((QPD_GSWZ >> bit) & 1) {
+                    sx |= hx << bit;
+                    sy |= hy << bit;
+                }
+            X ^= sx;
+            Y ^= sy;
+        }
     }
-    uint32_t out = 0;
+    uint32_t idx[NE];
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
         const int j = k >> 1;
         const uint32_t W = (k & 1) ? Y : X;
-        uint32_t idx;
         if constexpr (ISG)  // byte 0 = byte j of W, byte 1 = byte j of the u bits, bytes 2-3 = 0
-            idx = __builtin_amdgcn_perm((k & 1) ? hy : hx, W, (uint32_t)(j | ((4 + j) << 8) | (0x0C << 16) | (0x0C << 24)));
+            idx[k] = __builtin_amdgcn_perm((k & 1) ? hy : hx, W, (uint32_t)(j | ((4 + j) << 8) | (0x0C << 16) | (0x0C << 24)));
         else
-            idx = __builtin_amdgcn_ubfe(W, 8 * j, 8);
-        out |= (uint32_t)tb[idx] << (4 * k);
+            idx[k] = __builtin_amdgcn_ubfe(W, 8 * j, 8);
+#if QPD_EXP_LUTMASK != 0xFFFF
+        idx[k] &= QPD_EXP_LUTMASK;
+#endif
     }
+#if QPD_LUT_PACK2
+    if constexpr (NE == 8) {
+        // The even elements' bytes as [e0, e2, e4, e6] (16-bit pairs: the compiler
+        // joins two loaded bytes with one v_perm), the odd ones' likewise, then one
+        // shift-or: about 8 VALU for the 8 results instead of a shift per element and
+        // an or3 per two.
+        typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+        const u16x2 r0 = {tb[idx[0]], tb[idx[4]]}, r1 = {tb[idx[2]], tb[idx[6]]};
+        const u16x2 s0 = {tb[idx[1]], tb[idx[5]]}, s1 = {tb[idx[3]], tb[idx[7]]};
+        const uint32_t E = __builtin_bit_cast(uint32_t, r0) | (__builtin_bit_cast(uint32_t, r1) << 8);
+        const uint32_t O = __builtin_bit_cast(uint32_t, s0) | (__builtin_bit_cast(uint32_t, s1) << 8);
+        return E | (O << 4);
+    }
+#endif
+    uint32_t out = 0;
+#pragma unroll
+    for (int k = 0; k < NE; ++k) out |= (uint32_t)tb[idx[k]] << (4 * k);
     return out;
 }
 
@@ -458,7 +519,7 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
 #pragma unroll
                     for (int k = 0; k < 4; ++k)
                         M[s].st(dl, op.dst_row + w0 + k, lane,
-                                LT ? lut_lds<8, ISG>(tb, A[s][k], B[s][k], ub[s] >> (k << 3))
+                                LT ? lut_lds<8, ISG>(A[s][k], B[s][k], ub[s] >> (k << 3))
                                    : lut_vec<8>(T, A[s][k], B[s][k], ub[s] >> (k << 3)));
             }
         } else {
@@ -499,7 +560,7 @@ __device__ __forceinline__ void fg_op(const FastPlan &P, const Mem (&M)[NS], con
             for (int k = 0; k < 4; ++k)
                 if (k < nwo)
                     M[s].st(dl, op.dst_row + k, lane,
-                            LT ? lut_lds<8, ISG>(tb, A[s][k], B[s][k], ub[s] >> (k << 3))
+                            LT ? lut_lds<8, ISG>(A[s][k], B[s][k], ub[s] >> (k << 3))
                                : lut_vec<8>(T, A[s][k], B[s][k], ub[s] >> (k << 3)));
     } else {  // ctemp in {2, 4}: the whole depth-d node (a then b) is one word
         uint32_t W[NS], ub[NS];
@@ -549,14 +610,14 @@ __device__ __forceinline__ void ff_op(const Mem (&M)[NS], const MOp &op, const i
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int w = (k < 2 ? 0 : nwc) + u0 + (k & 1);
-                X[s][k] = lut_lds<8, ISG>(tb, A[s][k], B[s][k], ub[s][k >> 1] >> ((w & 3) << 3));
+                X[s][k] = lut_lds<8, ISG>(A[s][k], B[s][k], ub[s][k >> 1] >> ((w & 3) << 3));
                 M[s].st(DL != 0, op.dst_row + w, lane, X[s][k]);
             }
 #pragma unroll
         for (int s = 0; s < NS; ++s)
 #pragma unroll
             for (int k = 0; k < 2; ++k)
-                M[s].st(CDL != 0, op.r_row + u0 + k, lane, lut_lds<8, false>(tb + 512, X[s][k], X[s][k + 2], 0u));
+                M[s].st(CDL != 0, op.r_row + u0 + k, lane, lut_lds<8, false, 512>(X[s][k], X[s][k + 2], 0u));
     }
 }
 
@@ -1175,13 +1236,13 @@ __device__ __forceinline__ void bot3_op(const FastPlan &P, const Mem (&M)[NS], c
         // The depth n-4 parent's f / g (SCLLUTDecoder.cpp:83-89 / :157-164,
         // ctemp = 8) folded in: W3 from the parent's 16 symbols, in registers.
         const bool sl = op.flags & MF_SRC_LDS, ul = op.flags & MF_U_LDS;
-        if constexpr (LT) stage_tab(tb, T2, (op.flags & MF_BG) ? lane : (lane & 31));
+        if constexpr (LT) stage_tab(tb, T2, (op.flags & MF_BG) ? gtab_dw(lane) : (lane & 31));
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             const int src = gbase + pfield(st[s].ps, op.sh_src);
             const uint32_t a = M[s].ld(sl, op.src_row, src), b = M[s].ld(sl, op.src_row + 1, src);
             const uint32_t ub = (op.flags & MF_BG) ? M[s].ld(ul, op.u_row, gbase + pfield(st[s].U(), op.sh_u)) : 0u;
-            x[s][0] = LT ? lut_lds<8, true>(tb, a, b, ub) : lut_vec<8>(T2, a, b, ub);  // (ub = 0 for f: entries < 256)
+            x[s][0] = LT ? lut_lds<8, true>(a, b, ub) : lut_vec<8>(T2, a, b, ub);  // (ub = 0 for f: entries < 256)
         }
     } else {
 #pragma unroll
@@ -1481,13 +1542,13 @@ __device__ __forceinline__ void botx_op(const FastPlan &P, const Mem (&M)[NS], c
 #endif
     if (op.flags & MF_BFG) {  // the depth n-4 parent's f / g folded in (as bot3_op)
         const bool sl = op.flags & MF_SRC_LDS, ul = op.flags & MF_U_LDS;
-        if constexpr (LT) stage_tab(tb, T2, (op.flags & MF_BG) ? lane : (lane & 31));
+        if constexpr (LT) stage_tab(tb, T2, (op.flags & MF_BG) ? gtab_dw(lane) : (lane & 31));
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             const int src = gbase + pfield(st[s].ps, op.sh_src);
             const uint32_t a = M[s].ld(sl, op.src_row, src), b = M[s].ld(sl, op.src_row + 1, src);
             const uint32_t ub = (op.flags & MF_BG) ? M[s].ld(ul, op.u_row, gbase + pfield(st[s].U(), op.sh_u)) : 0u;
-            x[s][0] = LT ? lut_lds<8, true>(tb, a, b, ub) : lut_vec<8>(T2, a, b, ub);
+            x[s][0] = LT ? lut_lds<8, true>(a, b, ub) : lut_vec<8>(T2, a, b, ub);
         }
     } else {
 #pragma unroll
@@ -1721,7 +1782,7 @@ __device__ __forceinline__ uint32_t spec_in(const Mem &M, const MOp &op, int src
     if (!(op.flags & MF_SFG)) return M.ld(sl, op.src_row + w, src);
     const uint32_t a = M.ld(sl, op.src_row, src), b = M.ld(sl, op.src_row + 1, src);
     const uint32_t ub = (op.flags & MF_SGG) ? M.ld(op.flags & MF_U_LDS, op.u_row, usrc) : 0u;
-    return LT ? lut_lds<8, true>(tb, a, b, ub) : lut_vec<8>(T2, a, b, ub);  // (f: ub = 0, entries < 256)
+    return LT ? lut_lds<8, true>(a, b, ub) : lut_vec<8>(T2, a, b, ub);  // (f: ub = 0, entries < 256)
 }
 
 // A special node's result word(s) `res` to its destination; MF_SCOMB (size 8):
@@ -1912,7 +1973,7 @@ __device__ __forceinline__ void r1_multi(const FastPlan &P, const Mem (&Mv)[NS],
     const bool uni = !GEN || (op.flags & MF_VUNI);
     const double vrow = uni && (lane & 15) < v ? vq[lane & 15] : 0.0;
     if constexpr (LT)
-        if (op.flags & MF_SFG) stage_tab(tb, T2, (op.flags & MF_SGG) ? lane : (lane & 31));
+        if (op.flags & MF_SFG) stage_tab(tb, T2, (op.flags & MF_SGG) ? gtab_dw(lane) : (lane & 31));
     R1Prep pr[NS];
 #pragma unroll 1
     for (int s = 0; s < NS; ++s) {  // set s in slot 0 (rotate_sets)
@@ -1995,7 +2056,7 @@ __device__ __forceinline__ void r0rep_multi(const FastPlan &P, const Mem (&Mv)[N
     }
     const int n8 = (temp + 7) >> 3;
     if constexpr (LT)
-        if (fl & MF_SFG) stage_tab(tb, T2, (fl & MF_SGG) ? lane : (lane & 31));
+        if (fl & MF_SFG) stage_tab(tb, T2, (fl & MF_SGG) ? gtab_dw(lane) : (lane & 31));
     typedef double d2 __attribute__((ext_vector_type(2)));
     d2 *const qt = (d2 *)(tb + 512);  // (LT, !GEN) the symbols' terms, after the f / g tables' 512 B
     if constexpr (LT && !GEN) {
@@ -2295,7 +2356,7 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
 #define QPD_WPE3 3
 #endif
 #ifndef QPD_WPE_W16
-#define QPD_WPE_W16 4  // SCL-LUT at 9 <= L <= 16 (W16)
+#define QPD_WPE_W16 5  // SCL-LUT at 9 <= L <= 16 (W16): 5.15 M frames/s at L = 16 vs 5.03 at 4, 4.49 at 3 (r06d)
 #endif
 // NS frame sets per wave (see above); L8: list decoders with L = 8; W16: SCL-LUT with
 // 9 <= L <= 16 (lane groups of 16, select_survivors16).
@@ -2330,17 +2391,22 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
     // (build_fast; +1.1 % SCL-LUT, -1.3 % when FastSCL-LUT's dropped them too, r05z5)
     constexpr bool kChan = !(PW1 && KIND == K_SCL_LUT);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
-    // rows of all sets interleaved, each set's selection scratch as its next two
-    // rows: set s's slots at sel_all + s * 64, its junk slots NS * 64 words on
-    const int sstride = 64;
-    int *const sel_all = (int *)(lds_dyn + NS * P.lds_rows * 64);
-    // list kinds at two frame sets: the f / g ops' byte tables (stage_tab), 768 B after
-    // the selection scratch, and the folded descents (MF_FF)
+    // list kinds at two frame sets: the f / g ops' byte tables (stage_tab) and the
+    // folded descents (MF_FF), 768 B at the start of the wave's LDS -- a constant
+    // address, so that every byte-table lookup is a ds_read_u8 of its index with the
+    // table's place in the instruction's offset field (one VALU add per lookup less
+    // than from a base in a register); then the rows of all sets, interleaved, and
+    // each set's selection scratch as its next two rows (set s's slots at sel_all +
+    // s * 64, its junk slots NS * 64 words on)
 #ifndef QPD_EXP_NO_LDSTAB
 #define QPD_EXP_NO_LDSTAB 0  // A/B: the f / g lookups by ds_bpermute from the table register (no byte tables)
 #endif
     constexpr bool kLdsTab = kList && NS >= 2 && !QPD_EXP_NO_LDSTAB;
-    uint8_t *const tb = (uint8_t *)(sel_all + NS * kSelInts);
+    constexpr int kTabWords = kLdsTab ? 192 : 0;  // (qpd_capi.hip: lds_tab_bytes)
+    uint8_t *const tb = (uint8_t *)lds_dyn;
+    uint32_t *const lds_rows = lds_dyn + kTabWords;
+    const int sstride = 64;
+    int *const sel_all = (int *)(lds_rows + NS * P.lds_rows * 64);
     Mem Mv[NS];
     {
         uint32_t *const slab = P.scratch + (size_t)blockIdx.x * NS * P.glb_rows * 64;
@@ -2348,7 +2414,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
             __builtin_amdgcn_make_buffer_rsrc(slab, 0, NS * P.glb_rows * 256 * QPD_EXP_SLABMUL, 0x00020000);
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            Mv[s].lds = lds_dyn + s * 64;
+            Mv[s].lds = lds_rows + s * 64;
             Mv[s].gp = slab + s * 64;
             Mv[s].rs = rs;
             Mv[s].so = s * 256;
@@ -2371,7 +2437,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
         // Diagnosis builds only: every LDS word and slab row of this wave set to
         // QPD_POISON at the start of each task, so that a read of a row no op of
         // this task wrote shows up as a parity difference.
-        for (int i = threadIdx.x; i < NS * (P.lds_rows * 64 + kSelInts); i += 64) lds_dyn[i] = (uint32_t)QPD_POISON;
+        for (int i = threadIdx.x; i < NS * (P.lds_rows * 64 + kSelInts); i += 64) lds_rows[i] = (uint32_t)QPD_POISON;
         for (int r = 0; r < NS * P.glb_rows; ++r) Mv[0].gp[r * 64 + threadIdx.x] = (uint32_t)QPD_POISON;
         wave_sync();
 #endif
@@ -2439,7 +2505,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                         return;
                     }
                     if (op.type == OP_R1 && (op.cnt <= stl::kThreshold || (fl & MF_R1_LDS)) && !(QPD_EXP_FSCL & 1024)) {
-                        r1_multi<kLdsTab, R1L>(P, Mv, op, stv, sel_all, sstride, gl, gbase, lane, lds_dyn, cur.T2, tb);
+                        r1_multi<kLdsTab, R1L>(P, Mv, op, stv, sel_all, sstride, gl, gbase, lane, lds_rows, cur.T2, tb);
                         return;
                     }
                     // without R1L every R1 node of > 16 elements has its LDS tail (the host
@@ -2451,14 +2517,14 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
 #pragma unroll 1
                   for (int s = 0; s < NS; ++s) {
                     special_op<kList, L8, R1L>(P, Mv[0].set(s), op, stv[0], sel_all + sstride * s, NS * sstride, gl, gbase,
-                                               L, lane, lds_dyn);
+                                               L, lane, lds_rows);
                     rotate_sets(stv);
                   }
 #else
 #pragma unroll
                   for (int s = 0; s < NS; ++s)
                     special_op<kList, L8, R1L>(P, Mv[s], op, stv[s], sel_all + sstride * s, NS * sstride, gl, gbase, L, lane,
-                                               lds_dyn);
+                                               lds_rows);
 #endif
               }
             };
@@ -2486,7 +2552,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                     if constexpr (kLdsTab) {
                         if (fl & MF_FF) {  // + the left child's f (fuse_descent)
                             const int key = ((fl & MF_DST_LDS) ? 1 : 0) | ((fl & MF_FF_DL) ? 2 : 0);
-                            stage_tab(tb, cur.T, op.type == OP_F ? (lane & 31) : lane);
+                            stage_tab(tb, cur.T, op.type == OP_F ? (lane & 31) : gtab_dw(lane));
                             stage_tab(tb + 512, cur.T2, lane & 31);
 #define QPD_FF(G, D_, C_) ff_op<G, D_, C_, NS>(Mv, op, src, usrc, tb, lane)
                             if (op.type == OP_F) {
@@ -2510,7 +2576,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                         // row spaces of source and destination fixed per instantiation
                         const int key = ((fl & MF_SRC_LDS) ? 1 : 0) | ((fl & MF_DST_LDS) ? 2 : 0);
                         if constexpr (kLdsTab)
-                            if (op.cnt >= 8) stage_tab(tb, cur.T, op.type == OP_F ? (lane & 31) : lane);
+                            if (op.cnt >= 8) stage_tab(tb, cur.T, op.type == OP_F ? (lane & 31) : gtab_dw(lane));
 #define QPD_FG(G, S_, D_) fg_op<G, true, NS, S_, D_, kLdsTab>(P, Mv, op, yv, src, usrc, cur.T, lane, tb)
                         // (S[d] in LDS puts S[d + 1] in LDS too: no key 1 variant)
                         if (op.type == OP_F) {
@@ -2695,7 +2761,14 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
 
         // Root partial sums -> u = x F^{(x)n} (FastSCLUT.cpp:186-198), R[0] rows;
         // output u[info] of the winning path (SCLLUTDecoder.cpp:244-252).
-        const int lane = threadIdx.x;
+        // FastSCL-LUT: the lane constants re-derived here too -- otherwise the compiler
+        // computes the tail's lane-dependent addresses once before the task loop and
+        // keeps them across the whole op loop in scratch (140 -> 80 B per lane, speed
+        // unchanged).  Not for SCL-LUT: there the same change raised the SGPR spills
+        // 148 -> 210 and cost 1.1 % (profiles/r06d_ab.txt); its scratch (112 B) is
+        // written once before the task loop and read once per task, in the tail.
+        int lane = threadIdx.x;
+        if constexpr (KIND == K_FASTSCL_LUT) asm volatile("" : "+v"(lane));
         const int gl = lane & (gs - 1);
         const int gbase = lane & ~(gs - 1);
         const bool rl = P.R0_lds;

@@ -343,6 +343,9 @@ class Engine {
                 continue;
             }
             fg_node<ISG>(op, srow(src, d), ISG ? urow(us, d + 1) : nullptr, srow_w(i, d + 1));
+#ifdef QPD_HOST_FG_ELEMS
+            QPD_HOST_FG_ELEMS(op, ISG, i, srow(src, d), ISG ? urow(us, d + 1) : nullptr);  // diagnostic builds
+#endif
             PS(i, d + 1) = (uint8_t)i;
         }
     }
