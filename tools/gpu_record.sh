@@ -23,4 +23,7 @@ step prof_fscl bash tools/profile_round.sh ${TAG}_fscl --kind FastSCL-LUT
 step bench timeout -k 10 300 python bench.py
 step bench_fscl timeout -k 10 300 python bench.py --kind FastSCL-LUT
 step mc timeout -k 10 300 python bench.py --mc-frames 1e8 --no-cpu-baseline
+# the fast engine's lane groups of 16 (SCL-LUT at L = 16) and BASELINE config C2
+step bench_l16 timeout -k 10 300 python bench.py --L 16 --frames 1048576 --no-e2e
+step bench_c2 timeout -k 10 300 python bench.py --kind SC-LUT --N 128 --K 32 --frames 16777216 --no-e2e
 echo "record $TAG done"
