@@ -1355,15 +1355,18 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
         int rc = upload(d->mops, mops.data(), mops.size(), d->hs);
         if (rc) return rc;
     }
-    // nibble-packed tables: entry (u, a, b) of node p at bit 4*(idx&7) of dword idx>>3
+    // nibble-packed tables: entry (u, a, b) of node p at bit 4*(idx&7) of dword idx>>3, idx =
+    // u * 256 + a * 16 + b; the leaf pairs' nodes (depth n-1: only the leaf lookups read them)
+    // transposed, idx = u * 256 + b * 16 + a (qpd_fast.hip leaf_idx, QPD_LEAF_T)
     std::vector<uint32_t> ft((size_t)(N - 1) * 32, 0), gt((size_t)(N - 1) * 64, 0);
     const size_t vv = (size_t)v * v;
     for (int p = 0; p < N - 1; ++p) {
         const uint8_t *tf = c->lut_f + (size_t)c->f_base[p] * vv;
         const uint8_t *tg = c->lut_g + (size_t)c->g_base[p] * 2 * vv;
+        const bool leafpair = QPD_LEAF_T && p >= (N >> 1) - 1;
         for (int a = 0; a < v; ++a)
             for (int b = 0; b < v; ++b) {
-                const int idx = a * 16 + b;
+                const int idx = leafpair ? b * 16 + a : a * 16 + b;
                 ft[(size_t)p * 32 + (idx >> 3)] |= (uint32_t)tf[a * v + b] << (4 * (idx & 7));
                 for (int u = 0; u < 2; ++u) {
                     const int gi = u * 256 + idx;

@@ -776,6 +776,13 @@ __device__ __forceinline__ uint64_t dmax_bits(uint64_t a, uint64_t b) {
     return __builtin_bit_cast(uint64_t, r);
 }
 
+// max(-x, 0) in one v_max_f64 (the builtin would canonicalize its operand first).
+__device__ __forceinline__ double neg_max0(double x) {
+    double r;
+    asm("v_max_f64 %0, -%1, 0" : "=v"(r) : "v"(x));
+    return r;
+}
+
 // Identity test of the L = 8 survivor selection, for every lane group of the
 // wave at once: the keeps K_j (this lane's keep key) are already in stable
 // order (K_0 <= ... <= K_7) and no flip F_j beats the largest keep (a flip
@@ -1109,9 +1116,9 @@ __device__ __forceinline__ void leaf_decide(Path (&st)[NS], const double (&dm)[N
     if (frozen) {
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            // :100-104, |dm|·(dm<0) as a select: the same double (|dm|·1 = |dm|,
-            // |dm|·0 = +0, and pm is never -0)
-            st[s].pm += dm[s] < 0 ? fabs(dm[s]) : 0.0;
+            // :100-104, |dm|·(dm<0) = max(-dm, 0): the same double (|dm|·1 = |dm| for
+            // dm < 0; otherwise +0, or -0 for dm = +0, and pm + -0 = pm: pm is never -0)
+            st[s].pm += neg_max0(dm[s]);
             dec[s] = 0u;
         }
         return;
@@ -1130,6 +1137,24 @@ __device__ __forceinline__ void leaf_decide(Path (&st)[NS], const double (&dm)[N
 // 2 symbols) | bL (bit 24, left leaf decision) | c2 (bits 25-26, left result
 // at depth n-1) | c3 (bits 27-30, left result at depth n-2).
 // ---------------------------------------------------------------------------
+// Leaf lookups (the depth n-1 node's f / g table, lut4) of the leaf pair whose
+// symbols a, b are nibbles 4, 5 of x1 (and, for g, the left decision u bit 24):
+// QPD_LEAF_T = 1 -- the host stores the depth n-1 tables transposed (entry
+// u * 256 + b * 16 + a, fast_tables in qpd_capi.hip), so the index is x1's
+// bits 16..23 (..24) as they lie: one field extract instead of two extracts, a
+// shift and an or per leaf.
+#ifndef QPD_LEAF_T
+#define QPD_LEAF_T 1
+#endif
+__device__ __forceinline__ uint32_t leaf_idx(uint32_t x1) {
+    if constexpr (QPD_LEAF_T) return __builtin_amdgcn_ubfe(x1, 16, 8);
+    return (((x1 >> 16) & 15u) << 4) | ((x1 >> 20) & 15u);
+}
+__device__ __forceinline__ uint32_t leaf_idx_g(uint32_t x1) {  // with u = bit 24
+    if constexpr (QPD_LEAF_T) return __builtin_amdgcn_ubfe(x1, 16, 9);
+    return (((x1 >> 24) & 1u) << 8) | leaf_idx(x1);
+}
+
 __device__ __forceinline__ uint32_t f_pair(uint32_t T, uint32_t hi, uint32_t w2) {  // 2 symbols of f(W2)
     return lut_vec<2>(T, w2, w2 >> 8, hi);
 }
@@ -1146,9 +1171,8 @@ __device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], u
     bool moved[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-        const uint32_t a = (x[s][1] >> 16) & 15u, b = (x[s][1] >> 20) & 15u;
         dm[s] = 0;
-        if (kList || !(fr & 1)) dm[s] = shfld(V, vo + (int)lut4(Tf, ((a << 4) | b) + fo));
+        if (kList || !(fr & 1)) dm[s] = shfld(V, vo + (int)lut4(Tf, leaf_idx(x[s][1]) + fo));
     }
 #if QPD_SPEC_RIGHT  // (SPEC: SCL-LUT; the FastSCL unit measured slower with it)
     // The right leaf's quanta for the decision the left leaf takes when its
@@ -1160,9 +1184,8 @@ __device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], u
     if constexpr (kList && LM == 8 && SPEC) {
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            const uint32_t a = (x[s][1] >> 16) & 15u, b = (x[s][1] >> 20) & 15u;
             const uint32_t hb = (fr & 1) ? 0u : (uint32_t)(dm[s] < 0);  // H4: SCL family `< 0`
-            sdm[s] = shfld(V, vo + 16 + (int)lut4(Tg, (hb << 8) | (a << 4) | b));
+            sdm[s] = shfld(V, vo + 16 + (int)lut4(Tg, (hb << 8) | leaf_idx(x[s][1])));
         }
     }
 #endif
@@ -1170,15 +1193,14 @@ __device__ __forceinline__ void bot_pair(Path (&st)[NS], uint32_t (&x)[NS][2], u
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         x[s][1] = (x[s][1] & ~(1u << 24)) | (bl[s] << 24);
-        const uint32_t a = (x[s][1] >> 16) & 15u, b = (x[s][1] >> 20) & 15u;
 #if QPD_SPEC_RIGHT
         if constexpr (kList && LM == 8 && SPEC) {
             dm[s] = sdm[s];
-            if (moved[s]) dm[s] = shfld(V, vo + 16 + (int)lut4(Tg, (bl[s] << 8) | (a << 4) | b));
+            if (moved[s]) dm[s] = shfld(V, vo + 16 + (int)lut4(Tg, leaf_idx_g(x[s][1])));
             continue;
         }
 #endif
-        if (kList || !(fr & 2)) dm[s] = shfld(V, vo + 16 + (int)lut4(Tg, (bl[s] << 8) | (a << 4) | b));
+        if (kList || !(fr & 2)) dm[s] = shfld(V, vo + 16 + (int)lut4(Tg, leaf_idx_g(x[s][1])));
     }
     leaf_decide<kList, LM>(st, dm, fr & 2, gl, gbase, L, lane, sel, sstride, x, br, moved);
 #pragma unroll
@@ -2613,7 +2635,7 @@ __global__ __launch_bounds__(64, NS == 3 ? QPD_WPE3
                         none[s][0] = 0;
                         if (kList || !frozen) {
                             const uint32_t W = sym_word<kChan>(P, Mv[s], op, yv[s], gbase + pfield(stv[s].ps, op.sh_src), 0, 2);
-                            uint32_t idx = ((W & 15u) << 4) | ((W >> 4) & 15u);
+                            uint32_t idx = QPD_LEAF_T ? (W & 0xFFu) : (((W & 15u) << 4) | ((W >> 4) & 15u));  // (leaf_idx)
                             if (right)
                                 idx |= (Mv[s].ld(fl & MF_U_LDS, op.u_row, gbase + pfield(stv[s].U(), op.sh_u)) & 1u) << 8;
                             dm[s] = shfld(cur.V, (int)lut4(cur.T, idx));  // vcl[n-1][k][s] (H3)
