@@ -105,14 +105,16 @@ struct qpd_decoder {
     int num_mops = 0;
     DeviceBuf pfx_mops;  // frozen-prefix stages' ops (lut_prefix_kernel): stage 1, then stage 2
     int pfx_nops = 0;    // stage 1 (one path per frame); 0: no split
+    int pfx1b_nops = 0;  // stage 1b (<= 2 live paths); 0: stage 2 resumes from stage 1
     int pfx2_nops = 0;   // stage 2 (<= 4 live paths); 0: the decode kernel resumes from stage 1
     int pfx_sets = 1;    // frame sets per wave of the prefix stages (QPD_PFX_SETS)
     int pfx1_rec = 0, pfx1_pm = 0;  // stage 1: words per record, metric word in it
-    int pfx2_rec = 0, pfx2_pm = 0;  // stage 2: words per path record, metric word in it
-    DeviceBuf pfx1_buf, pfx2_buf;   // the stages' records (interleaved, see FastPlan::pfx)
-    size_t pfx1_cap = 0, pfx2_cap = 0;
+    int pfx1b_rec = 0, pfx1b_pm = 0;  // stage 1b: words per path record, metric word in it
+    int pfx2_rec = 0, pfx2_pm = 0;    // stage 2: words per path record, metric word in it
+    DeviceBuf pfx1_buf, pfx1b_buf, pfx2_buf;  // the stages' records (interleaved, see FastPlan::pfx)
+    size_t pfx1_cap = 0, pfx1b_cap = 0, pfx2_cap = 0;
     std::vector<qpd::MOp> pfx_ops_host, main_ops_host;  // host copies of the split schedule (patch_imports)
-    const void *xin_at[2] = {nullptr, nullptr};         // the buffer addresses the device copies hold
+    const void *xin_at[3] = {nullptr, nullptr, nullptr};         // the buffer addresses the device copies hold
     std::vector<Op> ops_host;
     DeviceBuf lut_f, f_base, lut_g, g_base, vcl, ops, info_pos, scratch, err;
     DeviceBuf r_f, r_g, q_bnd, q_rec, bnd_off, bnd_len, rec_off, rec_len;  // float-domain re-quantizers
@@ -773,18 +775,22 @@ void op_rows(const qpd::MOp &m, Fn &&acc) {
 }
 
 // Frozen-prefix stages of an SCL schedule (see lut_prefix_kernel).
-//   stage 1: ops [0, s1) -- up to the first forking op: one path, gs = 1;
-//   stage 2: ops [s1, s2) -- up to the op with the third information leaf: at
-//            most 4 live paths, run with L = 4 (the stable selection keeps the
-//            live paths in slots 0-3 in the same order as with L = 8, and the
-//            other slots' metrics are infinite);
-//   decode:  ops [s2, end) with the full list.
+//   stage 1:  ops [0, s1) -- up to the first forking op: one path, gs = 1;
+//   stage 1b: ops [s1, sb) -- up to the op with the second information leaf: at
+//             most 2 live paths, run with L = 2, gs = 2 (opt-in: QPD_PFX1B=1);
+//   stage 2:  ops [sb, s2) -- up to the op with the third information leaf: at
+//             most 4 live paths, run with L = 4;
+//   decode:   ops [s2, end) with the full list.
+// For 2L <= 16 mink's sort is stable (SCLLUTDecoder.cpp:8-21, H1): the live
+// candidates (keeps before flips, each in slot order) take slots 0..2k-1 in the
+// same order at L = 2, 4 or 8, and the other slots' metrics are infinite.
 // Each stage ends with OP_EXPORT of the words the later ops read before
 // writing them (live-in) and begins with OP_IMPORT of its predecessor's.
 struct PrefixPlan {
-    std::vector<qpd::MOp> st1, st2, rest;
-    int rec1 = 0, pm1 = 0;  // stage 1: words per record, metric word in it
-    int rec2 = 0, pm2 = 0;  // stage 2: words per path record, metric word in it
+    std::vector<qpd::MOp> st1, st1b, st2, rest;
+    int rec1 = 0, pm1 = 0;    // stage 1: words per record, metric word in it
+    int rec1b = 0, pm1b = 0;  // stage 1b: words per path record, metric word in it
+    int rec2 = 0, pm2 = 0;    // stage 2: words per path record, metric word in it
 };
 
 bool is_fork(const qpd::MOp &m) {
@@ -902,37 +908,57 @@ bool plan_prefix(const std::vector<qpd::MOp> &ops, const FastOwner &own, int L, 
         pp.rest.insert(pp.rest.end(), ops.begin() + s1, ops.end());
         return true;
     }
-    // stage 2 -> four-path records (G = 4, PS = 2): every live word, read through the
-    // lineage's pointer of its depth, and the metric
+    // stage 2 -> four-path records (G = 4, PS = 2), stage 1b -> two-path records (G = 5,
+    // PS = 1): every live word, read through the lineage's pointer of its depth, and the metric
+    auto path_records = [&](const std::vector<char> (&live)[2], int G, int PS, int node, std::vector<MOp> &imp,
+                            std::vector<MOp> &exp, int &rec, int &pmw) {
+        int w = 0;
+        live_runs(live, own, [&](int sp, int r, int cnt, int slot, int dd) {
+            MOp x = blank_op(OP_EXPORT);
+            x.flags = (sp ? MF_SRC_LDS : 0) | (slot == 1 ? MF_VIA_PS : slot == 2 ? MF_VIA_PU : 0);
+            x.sh_src = 4 * dd;
+            x.src_row = r;
+            x.dst_row = w;
+            x.cnt = cnt;
+            exp.push_back(x);
+            MOp m = blank_op(OP_IMPORT);
+            m.flags = MF_XBUF | (sp ? MF_DST_LDS : 0);
+            m.src_row = w;
+            m.dst_row = r;
+            m.cnt = cnt;
+            imp.push_back(m);
+            w += cnt;
+        });
+        pmw = w;
+        rec = w + 2;
+        MOp pm = blank_op(OP_IMPORT);
+        pm.flags = MF_XBUF | MF_PM;
+        pm.src_row = pmw;
+        imp.insert(imp.begin(), pm);
+        for (MOp &m : imp) {
+            m.tab = rec;
+            m.vrow = G | (PS << 8);
+            m.tab2 = 1 << PS;  // live paths of the record
+            m.node = node;     // buffer: 2 stage 2's, 3 stage 1b's
+        }
+    };
     std::vector<MOp> imp2, exp2;
-    int w2 = 0;
-    live_runs(live2, own, [&](int sp, int r, int cnt, int slot, int dd) {
-        MOp x = blank_op(OP_EXPORT);
-        x.flags = (sp ? MF_SRC_LDS : 0) | (slot == 1 ? MF_VIA_PS : slot == 2 ? MF_VIA_PU : 0);
-        x.sh_src = 4 * dd;
-        x.src_row = r;
-        x.dst_row = w2;
-        x.cnt = cnt;
-        exp2.push_back(x);
-        MOp m = blank_op(OP_IMPORT);
-        m.flags = MF_XBUF | (sp ? MF_DST_LDS : 0);
-        m.src_row = w2;
-        m.dst_row = r;
-        m.cnt = cnt;
-        imp2.push_back(m);
-        w2 += cnt;
-    });
-    pp.pm2 = w2;
-    pp.rec2 = w2 + 2;
-    MOp pm2 = blank_op(OP_IMPORT);
-    pm2.flags = MF_XBUF | MF_PM;
-    pm2.src_row = pp.pm2;
-    imp2.insert(imp2.begin(), pm2);
-    for (MOp &m : imp2) {
-        m.tab = pp.rec2;
-        m.vrow = 4 | (2 << 8);
-        m.tab2 = 4;
-        m.node = 2;  // buffer: stage 2's
+    path_records(live2, 4, 2, 2, imp2, exp2, pp.rec2, pp.pm2);
+    // stage 1b (opt-in, QPD_PFX1B=1): the ops up to the one with the second information
+    // leaf, run by 2 lanes per frame instead of stage 2's 4 (a third of the stages' lane
+    // lookups on the bench code).  Measured -0.7 % on the bench workload: stage 2 2.19 ->
+    // 1.30 ms, but stage 1b's own launch, drain and records take 1.07 ms (profiles/r06m_*).
+    size_t sb = s1;
+    for (int inf = 0; sb < ops.size() && inf + info_leaves(ops[sb]) <= 1; ++sb) inf += info_leaves(ops[sb]);
+    std::vector<char> liveb[2];
+    if (sb > s1 && sb < s2 && getenv("QPD_PFX1B") && live_in(ops, sb, own, liveb)) {
+        std::vector<MOp> impb, expb;
+        path_records(liveb, 5, 1, 3, impb, expb, pp.rec1b, pp.pm1b);
+        pp.st1b = imp1;
+        pp.st1b.insert(pp.st1b.end(), ops.begin() + s1, ops.begin() + sb);
+        pp.st1b.insert(pp.st1b.end(), expb.begin(), expb.end());
+        imp1 = impb;  // stage 2 starts from stage 1b's records
+        s1 = sb;
     }
     pp.st2 = imp1;
     pp.st2.insert(pp.st2.end(), ops.begin() + s1, ops.begin() + s2);
@@ -942,15 +968,15 @@ bool plan_prefix(const std::vector<qpd::MOp> &ops, const FastOwner &own, int L, 
     return true;
 }
 
-// Point the import ops of a prefix-split schedule at the stage buffers (op.node: 1 / 2),
-// on the launch stream, when a buffer moved.
+// Point the import ops of a prefix-split schedule at the stage buffers (op.node: 1 / 2 /
+// 3 = stage 1b), on the launch stream, when a buffer moved.
 int patch_imports(qpd_decoder *d, hipStream_t st) {
-    const void *b1 = d->pfx1_buf.p, *b2 = d->pfx2_buf.p;
-    if (d->xin_at[0] == b1 && d->xin_at[1] == b2) return QPD_OK;
+    const void *b1 = d->pfx1_buf.p, *b2 = d->pfx2_buf.p, *b3 = d->pfx1b_buf.p;
+    if (d->xin_at[0] == b1 && d->xin_at[1] == b2 && d->xin_at[2] == b3) return QPD_OK;
     auto patch = [&](std::vector<qpd::MOp> &v) {
         for (qpd::MOp &m : v)
             if (m.type == qpd::OP_IMPORT && (m.flags & qpd::MF_XBUF)) {
-                const uint64_t a = (uint64_t)(uintptr_t)(m.node == 2 ? b2 : b1);
+                const uint64_t a = (uint64_t)(uintptr_t)(m.node == 3 ? b3 : m.node == 2 ? b2 : b1);
                 m.u_row = (int32_t)(uint32_t)a;
                 m.r_row = (int32_t)(uint32_t)(a >> 32);
             }
@@ -963,6 +989,7 @@ int patch_imports(qpd_decoder *d, hipStream_t st) {
                            hipMemcpyHostToDevice, st));
     d->xin_at[0] = b1;
     d->xin_at[1] = b2;
+    d->xin_at[2] = b3;
     return QPD_OK;
 }
 
@@ -1308,15 +1335,18 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
         if (d->sets == 2) fuse_descent(mops);
         if (d->pfx_sets == 2) {
             fuse_descent(pp.st1);
+            fuse_descent(pp.st1b);
             fuse_descent(pp.st2);
         }
     }
     if (list_kind && !getenv("QPD_NO_BC2")) {  // folded depth n-5 combines (any NS)
         fold_combine(mops);
         fold_combine(pp.st1);
+        fold_combine(pp.st1b);
         fold_combine(pp.st2);
     }
     place_syncs(pp.st1, true);
+    place_syncs(pp.st1b, true);
     place_syncs(pp.st2, true);
     place_syncs(mops, c->kind == QPD_SCL_LUT || c->kind == QPD_FASTSCL_LUT);
     // one pointer word: the list kinds at one or two frame sets (the instantiations
@@ -1332,14 +1362,18 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
             d->r1l = true;
     // (SCL-LUT only with the root pre-pass: those kernels have no channel reads, lut_fast_kernel kChan)
     const bool pw1_ok = c->kind == QPD_SCL_LUT ? NS <= 2 && Ly.pre : (c->kind == QPD_FASTSCL_LUT && NS == 2 && d->l8 && !d->r1l);
-    if (pw1_ok && !getenv("QPD_NO_PW1")) d->pw1 = compact_pointer_fields({&mops, &pp.st1, &pp.st2});
+    if (pw1_ok && !getenv("QPD_NO_PW1")) d->pw1 = compact_pointer_fields({&mops, &pp.st1, &pp.st1b, &pp.st2});
     d->pfx_nops = (int)pp.st1.size();
+    d->pfx1b_nops = (int)pp.st1b.size();
     d->pfx2_nops = (int)pp.st2.size();
     d->pfx1_rec = pp.rec1;
     d->pfx1_pm = pp.pm1;
+    d->pfx1b_rec = pp.rec1b;
+    d->pfx1b_pm = pp.pm1b;
     d->pfx2_rec = pp.rec2;
     d->pfx2_pm = pp.pm2;
-    d->pfx_ops_host = pp.st1;  // one device array: stage 1, then stage 2
+    d->pfx_ops_host = pp.st1;  // one device array: stage 1, stage 1b, then stage 2
+    d->pfx_ops_host.insert(d->pfx_ops_host.end(), pp.st1b.begin(), pp.st1b.end());
     d->pfx_ops_host.insert(d->pfx_ops_host.end(), pp.st2.begin(), pp.st2.end());
     if (!d->pfx_ops_host.empty()) {
         int rc = upload(d->pfx_mops, d->pfx_ops_host.data(), d->pfx_ops_host.size(), d->hs);
@@ -1350,7 +1384,7 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
         if ((m.type == qpd::OP_F || m.type == qpd::OP_G) && (m.flags & qpd::MF_SRC_LDS) && !(m.flags & qpd::MF_DST_LDS))
             return fail(QPD_E_INVALID, "fast plan: an f/g op reads LDS rows and writes slab rows");
     F.nops = (int)mops.size();
-    d->num_mops = F.nops + d->pfx_nops + d->pfx2_nops;
+    d->num_mops = F.nops + d->pfx_nops + d->pfx1b_nops + d->pfx2_nops;
     {
         int rc = upload(d->mops, mops.data(), mops.size(), d->hs);
         if (rc) return rc;
@@ -1722,7 +1756,7 @@ int qpd_get_info(const qpd_decoder *d, qpd_info *info) {
     info->engine = d->engine;
     info->lds_bytes_per_wave = d->lds_bytes;
     info->lds_from_depth = d->engine == QPD_ENGINE_FAST ? d->fplan.lds_from : -1;
-    info->prefix_ops = d->engine == QPD_ENGINE_FAST ? d->pfx_nops + d->pfx2_nops : 0;
+    info->prefix_ops = d->engine == QPD_ENGINE_FAST ? d->pfx_nops + d->pfx1b_nops + d->pfx2_nops : 0;
     info->last_engine = d->last_engine;
     // f / g ops of a node at depth d look up N >> (d + 1) symbols each; a leaf
     // pair's two decisions one each (SCLLUTDecoder.cpp:83-89, :157-164)
@@ -1776,8 +1810,9 @@ int decode_pre_rows(qpd_decoder *d, const uint32_t *rows, int64_t Bc, uint8_t *o
     qpd::FastPlan fp = d->fplan;
     fp.in_vec = 1;
     fp.in_shift = fp.n - 2;
-    if (d->pfx_nops > 0) {  // the frozen-prefix stages (DESIGN.md §3.x), then the decode
+    if (d->pfx_nops > 0) {  // the frozen-prefix stages (DESIGN.md §3.3), then the decode
         int rc = ensure_records(d->pfx1_buf, d->pfx1_cap, Bc, d->pfx1_rec, 1);
+        if (!rc && d->pfx1b_nops > 0) rc = ensure_records(d->pfx1b_buf, d->pfx1b_cap, Bc, d->pfx1b_rec, 2);
         if (!rc && d->pfx2_nops > 0) rc = ensure_records(d->pfx2_buf, d->pfx2_cap, Bc, d->pfx2_rec, 4);
         if (!rc) rc = patch_imports(d, st);
         if (rc) return rc;
@@ -1793,8 +1828,21 @@ int decode_pre_rows(qpd_decoder *d, const uint32_t *rows, int64_t Bc, uint8_t *o
         pp.pm_off = d->pfx1_pm;
         rc = fast_launch(d, pp, (const int32_t *)rows, Bc, nullptr, st, true);
         if (rc) return rc;
-        if (d->pfx2_nops > 0) {  // stage 2: <= 4 live paths, L = 4
+        if (d->pfx1b_nops > 0) {  // stage 1b: <= 2 live paths, L = 2
             pp.ops = (const qpd::MOp *)d->pfx_mops.p + d->pfx_nops;
+            pp.nops = d->pfx1b_nops;
+            pp.gs = 2;
+            pp.fpw = 32;
+            pp.L = 2;
+            pp.pfx = (uint32_t *)d->pfx1b_buf.p;
+            pp.pfx_rec = d->pfx1b_rec;
+            pp.pfx_geo = 5 | (1 << 8);
+            pp.pm_off = d->pfx1b_pm;
+            rc = fast_launch(d, pp, (const int32_t *)rows, Bc, nullptr, st, true);
+            if (rc) return rc;
+        }
+        if (d->pfx2_nops > 0) {  // stage 2: <= 4 live paths, L = 4
+            pp.ops = (const qpd::MOp *)d->pfx_mops.p + d->pfx_nops + d->pfx1b_nops;
             pp.nops = d->pfx2_nops;
             pp.gs = 4;
             pp.fpw = 16;

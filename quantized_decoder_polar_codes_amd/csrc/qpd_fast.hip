@@ -856,11 +856,11 @@ __device__ __forceinline__ bool keep_all8(uint64_t K, uint64_t F, int gl) {
 //  * strict identity (keep_all16): keeps strictly increasing, every flip
 //    strictly above the largest keep -- the unique sorted order puts keep j in
 //    slot j whatever the algorithm;
-//  * select_survivors16: stable ranks (key, reference index) against the 15
-//    row partners by DPP row rotations, plus a tie flag; groups with a tie
-//    among their first L ranks replay stl::sort_small_prefix (the generic
-//    engine's replay, stl_sort.hpp) on their first lane over the set's
-//    selection scratch, one group after the other.
+//  * select_survivors16: dense key ranks against the 15 row partners by DPP
+//    row rotations, then every group replays libstdc++'s partitions
+//    (stl::partition_prefix, stl_sort.hpp) on its 2L ranks in parallel (scan-stop
+//    masks, swaps by ds_bpermute); only a group that reaches the introsort's
+//    depth limit replays stl::sort_small_prefix serially on its first lane.
 // Candidates are encoded keep j -> j, flip j -> 16 + j (flips after keeps, as
 // the reference's indices j < L <= L + j); lanes gl >= L are padding (+inf
 // keys, never scattered below L).

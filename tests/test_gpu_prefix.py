@@ -87,6 +87,32 @@ def test_prefix_equals_unsplit(kind, N, K, L, qpd, monkeypatch):
     assert np.array_equal(ga, gb), np.flatnonzero((ga != gb).any(1))[:10]
 
 
+@pytest.mark.parametrize("N,K,L", [(1024, 512, 8), (512, 256, 8), (1024, 384, 6)])
+def test_prefix_stage1b(N, K, L, qpd, oracle_mod, monkeypatch):
+    """Stage 1b (2 live paths at L = 2) on tie-heavy tables (3 distinct quanta
+    magnitudes, all-equal symbol frames: the L = 2 forks see tied keeps and
+    flips): the bits equal the default split (no stage 1b), the unsplit kernel
+    and the oracle."""
+    fm, nt = _code(N, K)
+    p = _tables(N, 500 + N + K + L)
+    rng = np.random.default_rng(N * K + L)
+    sym = rng.integers(0, 16, size=(2053, N), dtype=np.int32)
+    sym[:256] = 7
+    sym[256:1024] = np.clip(sym[256:1024] // 2 + 8, 0, 15)
+    monkeypatch.setenv("QPD_PFX1B", "1")
+    a = _make(qpd, monkeypatch, "SCL-LUT", p, K, fm, L, nt, True)
+    monkeypatch.delenv("QPD_PFX1B", raising=False)
+    c = _make(qpd, monkeypatch, "SCL-LUT", p, K, fm, L, nt, True)
+    b = _make(qpd, monkeypatch, "SCL-LUT", p, K, fm, L, nt, False)
+    assert a.info()["prefix_ops"] > c.info()["prefix_ops"] > 0 == b.info()["prefix_ops"]  # stage 1b taken
+    ga, gc, gb = a.decode_batch(sym), c.decode_batch(sym), b.decode_batch(sym)
+    assert np.array_equal(ga, gc), np.flatnonzero((ga != gc).any(1))[:10]
+    assert np.array_equal(ga, gb), np.flatnonzero((ga != gb).any(1))[:10]
+    rows = np.r_[0:40, 256:296, 1024:1064]
+    want = oracle_mod.decode_lut("SCL-LUT", p, K, L, fm, sym[rows], node_type=nt)
+    assert_frames_equal(ga[rows], want, a, f"prefix-1b-{N}-{K}-{L}")
+
+
 @pytest.mark.parametrize("N,K", [(64, 64), (1024, 1024), (1024, 16)])
 def test_prefix_edge_codes_exact(N, K, qpd, oracle_mod, monkeypatch):
     """Every bit information (K = N: the prefix is only the f ops down to the
