@@ -859,8 +859,8 @@ __device__ __forceinline__ bool keep_all8(uint64_t K, uint64_t F, int gl) {
 //  * select_survivors16: dense key ranks against the 15 row partners by DPP
 //    row rotations, then every group replays libstdc++'s partitions
 //    (stl::partition_prefix, stl_sort.hpp) on its 2L ranks in parallel (scan-stop
-//    masks, swaps by ds_bpermute); only a group that reaches the introsort's
-//    depth limit replays stl::sort_small_prefix serially on its first lane.
+//    masks, all of a partition's swaps at once); only a group that reaches the
+//    introsort's depth limit replays stl::sort_small_prefix serially on its first lane.
 // Candidates are encoded keep j -> j, flip j -> 16 + j (flips after keeps, as
 // the reference's indices j < L <= L + j); lanes gl >= L are padding (+inf
 // keys, never scattered below L).
@@ -984,30 +984,54 @@ __device__ __forceinline__ Sel select_survivors16(double kk, double kf, int gl, 
         // the array before the partition (from the left / from the right) while they
         // have not crossed; the scan that then runs on stops at the last right stop
         // at the latest (its swapped-in entry): cut = min(next left stop, last right stop).
+        // All swaps at once: every stop position learns its rank among the left /
+        // right stops (popcounts of the masks), publishes itself in the group's byte
+        // slots (left stops at [0, 32), right stops at [32, 64) of the set's selection
+        // scratch) and reads the stop of the same rank on the other side: the k-th pair
+        // swaps iff its left stop lies below its right stop (a prefix of the k), and a
+        // position is in at most one swapping pair.
         const uint32_t pv = em >> 5;
         const uint32_t in = ((l < 32 ? (1u << l) : 0u) - 1u) & ~((2u << f) - 1u);  // positions [f + 1, l)
         const uint32_t r0 = (E & 0xFFFFu) >> 5, r1 = E >> 21;
-        uint32_t GE = w16_mask(!pad && r0 >= pv, !pad && r1 >= pv, gbase, L) & in;
-        uint32_t LE = w16_mask(!pad && r0 <= pv, !pad && r1 <= pv, gbase, L) & in;
-        int a = GE ? __builtin_ctz(GE) : n2, b = LE ? 31 - __builtin_clz(LE) : -1, bprev = n2;
-        bool act = live && a < b;
-#pragma unroll 1
-        while (__builtin_amdgcn_ballot_w64(act)) {
-            const int pa = act ? a : 0, pb = act ? b : 0;
-            const uint32_t xa = w16_rd(E, gbase, L, pa), xb = w16_rd(E, gbase, L, pb);
-            if (act) {
-                E = w16_wr(E, gl, L, pa, xb);
-                E = w16_wr(E, gl, L, pb, xa);
-                GE &= GE - 1u;
-                LE &= ~(1u << pb);
-                bprev = pb;
-                a = GE ? __builtin_ctz(GE) : n2;
-                b = LE ? 31 - __builtin_clz(LE) : -1;
-                act = a < b;
+        const uint32_t GE = w16_mask(!pad && r0 >= pv, !pad && r1 >= pv, gbase, L) & in;
+        const uint32_t LE = w16_mask(!pad && r0 <= pv, !pad && r1 <= pv, gbase, L) & in;
+        uint8_t *const slot = (uint8_t *)sel + 4 * gbase;  // the group's 64 bytes
+        const int q[2] = {gl, L + gl};
+        int kA[2], kB[2];
+        bool ge[2], le[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            ge[h] = !pad && ((GE >> q[h]) & 1u);
+            le[h] = !pad && ((LE >> q[h]) & 1u);
+            kA[h] = __builtin_popcount(GE & ((1u << q[h]) - 1u));                      // rank from the left
+            kB[h] = __builtin_popcount(LE & ~((q[h] < 31 ? (2u << q[h]) : 0u) - 1u));  // rank from the right
+            if (live && ge[h]) slot[kA[h]] = (uint8_t)q[h];
+            if (live && le[h]) slot[32 + kB[h]] = (uint8_t)q[h];
+        }
+        lds_order();
+        const int nA = __builtin_popcount(GE), nB = __builtin_popcount(LE);
+        int part[2];
+        bool lsw[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            part[h] = q[h];
+            lsw[h] = false;
+            const int bk = ge[h] && kA[h] < nB ? slot[32 + kA[h]] : -1;  // this left stop's right partner
+            const int ak = le[h] && kB[h] < nA ? slot[kB[h]] : 64;       // this right stop's left partner
+            if (q[h] < bk) {
+                part[h] = bk;
+                lsw[h] = true;
+            } else if (ak < q[h]) {
+                part[h] = ak;
             }
         }
+        const int S = __builtin_popcount(w16_mask(lsw[0], lsw[1], gbase, L));  // swaps of this partition
+        const int cut_a = S < nA ? slot[S] : n2, cut_b = S >= 1 ? slot[32 + S - 1] : n2;
+        lds_order();
+        const uint32_t x0 = w16_rd(E, gbase, L, part[0]), x1 = w16_rd(E, gbase, L, part[1]);
+        if (live && !pad) E = x0 | (x1 << 16);
         if (live) {
-            const int cut = a < bprev ? a : bprev;
+            const int cut = cut_a < cut_b ? cut_a : cut_b;
             if (cut >= L && cut < end) end = cut;  // a block boundary past the first L positions
             if (l - cut > stl::kThreshold) {
                 if (cut >= end) live = false;  // the reference's recursion on [cut, l) lies past the prefix
@@ -2378,7 +2402,8 @@ __device__ __forceinline__ void special_op(const FastPlan &P, const Mem &M, cons
 #define QPD_WPE3 3
 #endif
 #ifndef QPD_WPE_W16
-#define QPD_WPE_W16 5  // SCL-LUT at 9 <= L <= 16 (W16): 5.15 M frames/s at L = 16 vs 5.03 at 4, 4.49 at 3 (r06d)
+#define QPD_WPE_W16 4  // SCL-LUT at 9 <= L <= 16 (W16): with the all-at-once swaps 5.27 M frames/s at L = 16
+                       // vs 5.09 for one swap per round at 4 or 5 waves (r06o; the swaps at 5: 4.52, spills)
 #endif
 // NS frame sets per wave (see above); L8: list decoders with L = 8; W16: SCL-LUT with
 // 9 <= L <= 16 (lane groups of 16, select_survivors16).

@@ -1,8 +1,9 @@
 // Scalar emulation of the W16 survivor selection (qpd_fast.hip select_survivors16:
 // dense key ranks, the group-parallel replay of stl::partition_prefix by scan-stop
-// masks and swaps, and the final (rank, position) selection), step for step as one
-// lane group runs it, checked against std::sort on the 2L candidate indices
-// (mink, SCLLUTDecoder.cpp:8-21) -- the first L outputs must be identical.
+// masks and all of a partition's swaps at once (stop ranks and slots), and the
+// final (rank, position) selection), step for step as one lane group runs it,
+// checked against std::sort on the 2L candidate indices (mink,
+// SCLLUTDecoder.cpp:8-21) -- the first L outputs must be identical.
 // Inputs: path-metric-like keys (keeps roughly ascending, flips = keep + penalty)
 // drawn from few distinct values (ties at almost every selection), all-equal and
 // +inf keys, and arrays that push the introsort toward its depth limit.
@@ -20,8 +21,6 @@ static int lg(int n) {
     while (n >>= 1) ++r;
     return r;
 }
-static int ctz(uint32_t x) { return __builtin_ctz(x); }
-static int hib(uint32_t x) { return 31 - __builtin_clz(x); }
 
 // Returns false when the replay needs its serial fallback (the depth limit).
 static bool emulate(const std::vector<double> &key, int L, std::vector<int> &out) {
@@ -56,16 +55,30 @@ static bool emulate(const std::vector<double> &key, int L, std::vector<int> &out
         }
         GE &= in;
         LE &= in;
-        int a = GE ? ctz(GE) : n2, b = LE ? hib(LE) : -1, bprev = n2;
-        while (a < b) {
-            std::swap(ent[a], ent[b]);
-            GE &= GE - 1u;
-            LE &= ~(1u << b);
-            bprev = b;
-            a = GE ? ctz(GE) : n2;
-            b = LE ? hib(LE) : -1;
+        // all swaps at once, as the kernel: ranks, byte slots, partners
+        int slotA[32], slotB[32];
+        for (int p = 0; p < n2; ++p) {
+            if ((GE >> p) & 1u) slotA[__builtin_popcount(GE & ((1u << p) - 1u))] = p;
+            if ((LE >> p) & 1u) slotB[__builtin_popcount(LE & ~((p < 31 ? (2u << p) : 0u) - 1u))] = p;
         }
-        const int cut = a < bprev ? a : bprev;
+        const int nA = __builtin_popcount(GE), nB = __builtin_popcount(LE);
+        std::vector<uint32_t> nxt(ent);
+        int S = 0;
+        for (int p = 0; p < n2; ++p) {
+            const int kA = __builtin_popcount(GE & ((1u << p) - 1u));
+            const int kB = __builtin_popcount(LE & ~((p < 31 ? (2u << p) : 0u) - 1u));
+            const int bk = ((GE >> p) & 1u) && kA < nB ? slotB[kA] : -1;
+            const int ak = ((LE >> p) & 1u) && kB < nA ? slotA[kB] : 64;
+            if (p < bk) {
+                nxt[p] = ent[bk];
+                ++S;
+            } else if (ak < p) {
+                nxt[p] = ent[ak];
+            }
+        }
+        ent = nxt;
+        const int cut_a = S < nA ? slotA[S] : n2, cut_b = S >= 1 ? slotB[S - 1] : n2;
+        const int cut = cut_a < cut_b ? cut_a : cut_b;
         if (cut >= L && cut < end) end = cut;
         if (l - cut > 16) {
             if (cut >= end) live = false;
