@@ -64,7 +64,8 @@ def parse(argv=None):
     ap.add_argument("--N", type=int, default=1024)
     ap.add_argument("--K", type=int, default=512)
     ap.add_argument("--L", type=int, default=8)
-    ap.add_argument("--frames", type=int, default=1 << 21, help="frames per GPU per step (one decode launch: 2^21 x 4 KB int32 symbols = 8 GB resident)")
+    ap.add_argument("--frames", type=int, default=1 << 23,
+                    help="frames per GPU per step (one decode launch: 2^23 x 4 KB int32 symbols = 32 GB resident)")
     ap.add_argument("--ebn0", type=float, default=2.0)
     ap.add_argument("--max-waves", type=int, default=0)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)

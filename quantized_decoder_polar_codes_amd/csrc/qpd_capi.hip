@@ -1294,7 +1294,11 @@ int build_fast(qpd_decoder *d, const qpd_config *c, const Schedule &s) {
     // decode launch ends in a drain where its SIMDs idle one by one, so fewer,
     // larger launches are faster -- SCL-LUT 35.9 / 37.5 / 38.3 M frames/s at
     // 2^18 / 2^20 / 2^21 frames per launch)
-    d->pre_chunk = std::max<int64_t>(1, ((int64_t)2 << 30) / N);
+    // <= 8 GB of rows per chunk (2^23 frames at N = 1024): one decode launch, one
+    // drain and one set of prefix-stage launches per 2^23 frames (SCL-LUT bench
+    // workload: 2 GB chunks 53.5 M frames/s at 2^22 frames per call, 4 GB 54.3 M;
+    // at 2^23 4 GB 54.8 M, 8 GB 55.2 M -- profiles/r06q_ab_chunk.txt)
+    d->pre_chunk = std::max<int64_t>(1, ((int64_t)8 << 30) / N);
     if (const char *e = getenv("QPD_PRE_CHUNK")) d->pre_chunk = std::max<int64_t>(1, atoll(e));
     fast_ops(mops, Ly, c->kind, N, n, v, c->frozen_bits, nt_fast, c->vcl, r1tab, 0, 0);
     if (r1tab.empty()) r1tab.push_back(0);

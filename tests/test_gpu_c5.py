@@ -23,7 +23,7 @@ pytestmark = pytest.mark.gpu
 N, K, L, EBN0 = 1024, 512, 8, 2.0
 FRAMES = 10 ** 8
 WORLD = 8
-BATCH = 1 << 21  # bench.py's frames per rank per step
+BATCH = 1 << 21  # frames per rank per step of the shards (bench.py used 2^21 through round 6 r06r)
 
 
 @pytest.fixture(scope="module")
