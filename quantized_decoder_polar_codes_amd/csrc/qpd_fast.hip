@@ -393,6 +393,9 @@ typedef __attribute__((address_space(3))) const uint8_t lds_u8;
 #ifndef QPD_LUT_PACK2
 #define QPD_LUT_PACK2 1  // lut_lds: the 8 results combined as 16-bit pairs (see there)
 #endif
+#ifndef QPD_LUT_OPAQUE
+#define QPD_LUT_OPAQUE 1  // lut_lds: the odd elements' word kept whole for the last shift-or (see there)
+#endif
 template <int NE, bool ISG, int TOFF = 0>
 __device__ __forceinline__ uint32_t lut_lds(uint32_t A, uint32_t B, uint32_t hi) {
     lds_u8 *const tb = (lds_u8 *)(size_t)TOFF;
@@ -431,13 +434,18 @@ __device__ __forceinline__ uint32_t lut_lds(uint32_t A, uint32_t B, uint32_t hi)
     if constexpr (NE == 8) {
         // The even elements' bytes as [e0, e2, e4, e6] (16-bit pairs: the compiler
         // joins two loaded bytes with one v_perm), the odd ones' likewise, then one
-        // shift-or: about 8 VALU for the 8 results instead of a shift per element and
-        // an or3 per two.
+        // shift-or: 7 VALU for the 8 results (4 v_perm, 3 v_lshl_or) instead of a
+        // shift per element and an or3 per two.  O passes through an empty asm so
+        // that the compiler does not distribute the final shift over O's two
+        // halves (v_lshlrev x2 + v_or3 instead of one v_lshl_or: +1 VALU per word).
         typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
         const u16x2 r0 = {tb[idx[0]], tb[idx[4]]}, r1 = {tb[idx[2]], tb[idx[6]]};
         const u16x2 s0 = {tb[idx[1]], tb[idx[5]]}, s1 = {tb[idx[3]], tb[idx[7]]};
         const uint32_t E = __builtin_bit_cast(uint32_t, r0) | (__builtin_bit_cast(uint32_t, r1) << 8);
-        const uint32_t O = __builtin_bit_cast(uint32_t, s0) | (__builtin_bit_cast(uint32_t, s1) << 8);
+        uint32_t O = __builtin_bit_cast(uint32_t, s0) | (__builtin_bit_cast(uint32_t, s1) << 8);
+#if QPD_LUT_OPAQUE
+        asm("" : "+v"(O));
+#endif
         return E | (O << 4);
     }
 #endif
