@@ -316,6 +316,13 @@ __device__ __forceinline__ uint32_t sym_word(const FastPlan &P, const Mem &M, co
 // one pass each derives the ds_bpermute byte address (idx >> 1, whose bits
 // 7:2 select the dword; + 128 for the upper half) and the nibble offset
 // ((idx & 7) * 4, used by v_bfe through its low 5 bits only).
+// QPD_VEC_CHAIN: lut_vec joins its results by one v_lshl_or per element (the
+// compiler otherwise shifts each and merges them with v_or3: +0.5 VALU per
+// lookup).  On in the FastSCL-LUT units (+0.5 %), off for SCL-LUT (-0.25 %:
+// the serial chain costs it latency), profiles/r06v_ab_vec_chain.txt.
+#ifndef QPD_VEC_CHAIN
+#define QPD_VEC_CHAIN 0
+#endif
 template <int NE>
 __device__ __forceinline__ uint32_t lut_vec(uint32_t T, uint32_t A, uint32_t B, uint32_t hi) {
     const uint32_t X = ((A << 4) & 0xF0F0F0F0u) | (B & 0x0F0F0F0Fu);
@@ -342,6 +349,9 @@ __device__ __forceinline__ uint32_t lut_vec(uint32_t T, uint32_t A, uint32_t B, 
         // ds_bpermute reads lane (addr >> 2) & 63: the bytes above j need no mask
         const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(WA >> (8 * j)), (int)T);
         out |= __builtin_amdgcn_ubfe(v, WS >> (8 * j), 4) << (4 * k);
+#if QPD_VEC_CHAIN
+        if (k + 1 < NE) asm("" : "+v"(out));  // one v_lshl_or per element, not shifts + v_or3
+#endif
     }
     return out;
 }

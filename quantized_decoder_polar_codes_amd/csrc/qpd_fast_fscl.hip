@@ -5,6 +5,9 @@
 // FastSCLLUTDecoder.cpp:82-213 and the mixed bottom subtrees (botx_op)
 // compiled in (KIND = K_FASTSCL_LUT).  See qpd_k_fast.hip for the units.
 #define QPD_FAST_TEMPLATES_ONLY
+#ifndef QPD_VEC_CHAIN  // lut_vec's results joined by one v_lshl_or each: FastSCL-LUT +0.5 %, SCL-LUT -0.25 % (r06v)
+#define QPD_VEC_CHAIN 1
+#endif
 #include "qpd_fast.hip"
 
 namespace qpd {

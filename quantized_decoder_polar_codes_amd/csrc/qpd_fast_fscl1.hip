@@ -2,6 +2,9 @@
 // path, two frame sets and L = 8 (lut_fast_kernel<K_FASTSCL_LUT, 2, true, false,
 // false, true>, qpd_fast.hip): the config-C4 bench kernel.  See qpd_k_fast.hip.
 #define QPD_FAST_TEMPLATES_ONLY
+#ifndef QPD_VEC_CHAIN  // lut_vec's results joined by one v_lshl_or each: FastSCL-LUT +0.5 %, SCL-LUT -0.25 % (r06v)
+#define QPD_VEC_CHAIN 1
+#endif
 #include "qpd_fast.hip"
 
 namespace qpd {
