@@ -1,7 +1,9 @@
 """Frozen-prefix split (lut_prefix_kernel, csrc/qpd_fast.hip): SCL-LUT (and
-CA-SCL-LUT) in pre-mode run the schedule up to the first information leaf once per frame and the
-decode kernel resumes from the exported rows and path metric.  The bits must
-equal the oracle's and the unsplit kernel's (QPD_NO_PFX=1) on every input:
+CA-SCL-LUT) in pre-mode run the schedule up to the first information leaf once
+per frame (stage 1), optionally to the second with 2 paths (stage 1b, L = 2,
+QPD_PFX1B=1) and to the third with 4 (stage 2, L = 4); the decode kernel
+resumes from the exported rows and path metrics.  The bits must equal the
+oracle's and the unsplit kernel's (QPD_NO_PFX=1) on every input:
   * PW codes at the bench size (split present) and odd batch sizes;
   * codes whose first bit is information (a prefix of f ops only) or whose
     prefix is most of the schedule;
