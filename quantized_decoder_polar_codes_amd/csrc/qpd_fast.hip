@@ -406,6 +406,9 @@ typedef __attribute__((address_space(3))) const uint8_t lds_u8;
 #ifndef QPD_LUT_OPAQUE
 #define QPD_LUT_OPAQUE 1  // lut_lds: the odd elements' word kept whole for the last shift-or (see there)
 #endif
+#ifndef QPD_LUT_OPAQUE_XY  // lut_lds: X, Y whole before the index extraction (-3 % static VALU; SCL-LUT +0.7 %,
+#define QPD_LUT_OPAQUE_XY 1  // FastSCL-LUT +0.9 %, profiles/r06za_ab_lut_xy.txt)
+#endif
 template <int NE, bool ISG, int TOFF = 0>
 __device__ __forceinline__ uint32_t lut_lds(uint32_t A, uint32_t B, uint32_t hi) {
     lds_u8 *const tb = (lds_u8 *)(size_t)TOFF;
@@ -427,6 +430,11 @@ __device__ __forceinline__ uint32_t lut_lds(uint32_t A, uint32_t B, uint32_t hi)
             Y ^= sy;
         }
     }
+#if QPD_LUT_OPAQUE_XY
+    // the words whole: otherwise the compiler rebuilds each index's byte from A and B
+    // (v_and + v_bitop3 chains) beside X / Y themselves -- 15 VALU for 8 f indices, not 12
+    asm("" : "+v"(X), "+v"(Y));
+#endif
     uint32_t idx[NE];
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
