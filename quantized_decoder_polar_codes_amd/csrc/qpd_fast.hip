@@ -1121,9 +1121,6 @@ __device__ __forceinline__ Sel select_survivors16(double kk, double kf, int gl, 
     return s;
 }
 
-#ifndef QPD_FORK_OPAQUE  // leaf_fork: the selection's lane terms behind the identity test (SCL-LUT +0.5 %,
-#define QPD_FORK_OPAQUE 1  // FastSCL-LUT +-0, scratch 104 -> 84 B; profiles/r06zc_ab_fork_opaque.txt)
-#endif
 // Info leaf with quanta dm: keep the L best of {keep, flip} candidates.
 // Returns the new decision; `extra` words follow the surviving lineage.
 // `moved` (wave-uniform): the selection was not the identity (paths moved).
@@ -1142,12 +1139,6 @@ __device__ __forceinline__ uint32_t leaf_fork(Path &st, double dm, int gl, int g
     if constexpr (LM == 16)
         if (keep_all16(__builtin_bit_cast(uint64_t, st.pm), __builtin_bit_cast(uint64_t, kf), gl, gbase, L)) return hd;
     moved = true;
-#if QPD_FORK_OPAQUE
-    // lane constants re-derived behind the identity test: otherwise the compiler
-    // computes the selection's lane terms (partner tie bits, scatter addresses)
-    // before the test, on every information leaf, identity or not
-    if constexpr (LM == 8) asm volatile("" : "+v"(gl), "+v"(gbase), "+v"(lane));
-#endif
     const Sel sl = LM == 8    ? select_survivors8(st.pm, kf, gl, gbase, lane, sel, sj)
                    : LM == 16 ? select_survivors16(st.pm, kf, gl, gbase, L, lane, sel, sj)
                               : select_survivors(st.pm, kf, gl, gbase, L, sel);
